@@ -1,0 +1,1424 @@
+// align_kernels.hip -- HIP (gfx950) kernels of the BWA-MEM alignment path behind bioseqdb's
+// nuclseq_search_bwa / nuclseq_multi_search_bwa (reference: bioseqdb/bwa.cpp:190-230, which calls
+// libbwa mem_align1 + mem_reg2aln).  The libbwa algorithm is re-expressed as five stage kernels over
+// device-resident index data; results must equal libbwa's bit for bit (checked against oracle/).
+//
+//   k_smem     mem_collect_intv   (bwt_smem1 x2 passes + bwt_seed_strategy1, sorted by info)
+//   k_chain    mem_chain + mem_chain_flt (SA lookups, kbtree with t = 5, klib introsort by weight)
+//   k_extend   mem_chain2aln (ksw_extend2) + mem_sort_dedup_patch (ksw_global2) + mem_mark_primary_se
+//   k_reg2aln  mem_reg2aln (infer_bw, bwa_gen_cigar2 / ksw_global2 traceback, clipping)
+//   k_pack     compaction of per-read slots into the bsq_hits layout
+//
+// Round-1 mapping: one read per lane (inter-task parallelism) with private scratch in HBM;
+// reads that overflow the small per-read slots are re-run by the host with large capacities.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bsq_device.h"
+#include "../../include/bsq.h"
+
+namespace bsq {
+
+#define DEV __device__ __forceinline__
+#define DEVN __device__ __noinline__
+
+// ------------------------------------------------------------------------------------------------
+// reference text access (bntseq.c _get_pac / bns_get_seq semantics)
+// ------------------------------------------------------------------------------------------------
+DEV int pac_get(const uint8_t *pac, int64_t i) { return (pac[i >> 2] >> ((~i & 3) << 1)) & 3; }
+// base of the forward+reverse text at coordinate p in [0, 2*l_pac)
+DEV int ref_at(const DIndex &ix, int64_t p)
+{
+    return p < ix.l_pac ? pac_get(ix.pac, p) : 3 - pac_get(ix.pac, (ix.l_pac << 1) - 1 - p);
+}
+
+// ------------------------------------------------------------------------------------------------
+// FM index: rank over the $-removed BWT (same function as libbwa bwt_occ4)
+// ------------------------------------------------------------------------------------------------
+DEV void occ_block(const OccBlock *blk, uint32_t r, uint64_t c[4])
+{
+    // counts of each base in the first r (1..128) rows of the block, added to the block prefix
+    const uint4 *p = reinterpret_cast<const uint4 *>(blk);
+    uint4 w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3];
+    uint64_t c0 = (uint64_t)w0.y << 32 | w0.x, c1 = (uint64_t)w0.w << 32 | w0.z;
+    uint64_t c2 = (uint64_t)w1.y << 32 | w1.x, c3 = (uint64_t)w1.w << 32 | w1.z;
+    uint64_t h0 = (uint64_t)w2.y << 32 | w2.x, h1 = (uint64_t)w2.w << 32 | w2.z;
+    uint64_t l0 = (uint64_t)w3.y << 32 | w3.x, l1 = (uint64_t)w3.w << 32 | w3.z;
+    uint64_t m0 = r >= 64 ? ~0ull : ((1ull << r) - 1);
+    uint64_t m1 = r >= 128 ? ~0ull : (r > 64 ? ((1ull << (r - 64)) - 1) : 0ull);
+    uint32_t n3 = __popcll(h0 & l0 & m0) + __popcll(h1 & l1 & m1);
+    uint32_t n2 = __popcll(h0 & ~l0 & m0) + __popcll(h1 & ~l1 & m1);
+    uint32_t n1 = __popcll(~h0 & l0 & m0) + __popcll(~h1 & l1 & m1);
+    c[0] = c0 + (r - n1 - n2 - n3);
+    c[1] = c1 + n1;
+    c[2] = c2 + n2;
+    c[3] = c3 + n3;
+}
+
+DEV void occ4(const DIndex &ix, uint64_t k, uint64_t c[4])
+{
+    if (k == (uint64_t)-1) { c[0] = c[1] = c[2] = c[3] = 0; return; }
+    k -= (k >= ix.primary);
+    occ_block(ix.occ + (k >> 7), (uint32_t)(k & 127) + 1, c);
+}
+
+// bwt_extend: both ranks (bwt_2occ4), one or two 64-B block fetches
+DEV void bwt_extend(const DIndex &ix, const Intv &ik, Intv ok[4], int is_back, uint64_t &nblk)
+{
+    uint64_t tk[4], tl[4];
+    const int nb = !is_back;
+    uint64_t k = ik.x[nb] - 1, l = ik.x[nb] - 1 + ik.x[2];
+    occ4(ix, k, tk);
+    occ4(ix, l, tl);
+    {
+        uint64_t kk = k == (uint64_t)-1 ? k : k - (k >= ix.primary), ll = l - (l >= ix.primary);
+        nblk += (k == (uint64_t)-1 || (kk >> 7) == (ll >> 7)) ? 1 : 2;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ok[i].x[nb] = ix.L2[i] + 1 + tk[i];
+        ok[i].x[2] = tl[i] - tk[i];
+    }
+    const int b = is_back;
+    ok[3].x[b] = ik.x[b] + (ik.x[nb] <= ix.primary && ik.x[nb] + ik.x[2] - 1 >= ix.primary);
+    ok[2].x[b] = ok[3].x[b] + ok[3].x[2];
+    ok[1].x[b] = ok[2].x[b] + ok[2].x[2];
+    ok[0].x[b] = ok[1].x[b] + ok[1].x[2];
+}
+
+DEV void set_intv(const DIndex &ix, int c, Intv &ik)
+{
+    ik.x[0] = ix.L2[c] + 1;
+    ik.x[2] = ix.L2[c + 1] - ix.L2[c];
+    ik.x[1] = ix.L2[3 - c] + 1;
+    ik.info = 0;
+}
+
+DEV uint64_t sa_at(const DIndex &ix, uint64_t row) { return ix.sa32 ? (uint64_t)ix.sa32[row] : ix.sa64[row]; }
+
+// ------------------------------------------------------------------------------------------------
+// bounded vectors in private scratch
+// ------------------------------------------------------------------------------------------------
+struct IV {
+    Intv *a;
+    int n, cap;
+    DEV bool push(const Intv &v, bool &ovf)
+    {
+        if (n >= cap) { ovf = true; return false; }
+        a[n++] = v;
+        return true;
+    }
+    DEV void reverse()
+    {
+        for (int j = 0; j < (n >> 1); ++j) { Intv t = a[n - 1 - j]; a[n - 1 - j] = a[j]; a[j] = t; }
+    }
+};
+
+// bwt_smem1a with max_intv = 0 (bwt_smem1)
+DEVN int smem1(const DIndex &ix, int len, const uint8_t *q, int x, int min_intv, IV &mem, IV &va, IV &vb,
+               bool &ovf, uint64_t &nblk)
+{
+    mem.n = 0;
+    if (q[x] > 3) return x + 1;
+    if (min_intv < 1) min_intv = 1;
+    IV *prev = &va, *curr = &vb;
+    Intv ik, ok[4];
+    set_intv(ix, q[x], ik);
+    ik.info = (uint64_t)(x + 1);
+    int i;
+    curr->n = 0;
+    for (i = x + 1; i < len; ++i) {
+        int qi = q[i];
+        if (qi < 4) {
+            int c = 3 - qi;
+            bwt_extend(ix, ik, ok, 0, nblk);
+            if (ok[c].x[2] != ik.x[2]) {
+                if (!curr->push(ik, ovf)) return len;
+                if (ok[c].x[2] < (uint64_t)min_intv) break;
+            }
+            ik = ok[c];
+            ik.info = (uint64_t)(i + 1);
+        } else {
+            if (!curr->push(ik, ovf)) return len;
+            break;
+        }
+    }
+    if (i == len && !curr->push(ik, ovf)) return len;
+    curr->reverse();
+    int ret = (int)curr->a[0].info;
+    { IV *t = curr; curr = prev; prev = t; }
+    for (i = x - 1; i >= -1; --i) {
+        int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+        curr->n = 0;
+        for (int j = 0; j < prev->n; ++j) {
+            Intv p = prev->a[j];
+            bool keep_hit;
+            if (c >= 0) {
+                bwt_extend(ix, p, ok, 1, nblk);
+                keep_hit = ok[c].x[2] < (uint64_t)min_intv;
+            } else keep_hit = true;
+            if (keep_hit) {
+                if (curr->n == 0) {
+                    if (mem.n == 0 || (uint64_t)(i + 1) < (mem.a[mem.n - 1].info >> 32)) {
+                        p.info |= (uint64_t)(i + 1) << 32;
+                        if (!mem.push(p, ovf)) return len;
+                    }
+                }
+            } else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
+                Intv t = ok[c];
+                t.info = p.info;
+                if (!curr->push(t, ovf)) return len;
+            }
+        }
+        if (curr->n == 0) break;
+        { IV *t = curr; curr = prev; prev = t; }
+    }
+    mem.reverse();
+    return ret;
+}
+
+DEV int seed_strategy1(const DIndex &ix, int len, const uint8_t *q, int x, int min_len, int max_intv, Intv &mem,
+                       uint64_t &nblk)
+{
+    Intv ik, ok[4];
+    mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
+    if (q[x] > 3) return x + 1;
+    set_intv(ix, q[x], ik);
+    for (int i = x + 1; i < len; ++i) {
+        int qi = q[i];
+        if (qi < 4) {
+            int c = 3 - qi;
+            bwt_extend(ix, ik, ok, 0, nblk);
+            if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
+                mem = ok[c];
+                mem.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
+                return i + 1;
+            }
+            ik = ok[c];
+        } else return i + 1;
+    }
+    return len;
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave-aggregated counter add (one atomic per wave and counter)
+// ------------------------------------------------------------------------------------------------
+DEV void wave_add(unsigned long long *dst, unsigned long long v)
+{
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
+DEV int read_of(const int32_t *sel, int i) { return sel ? sel[i] : i; }
+
+// ------------------------------------------------------------------------------------------------
+// k_smem: mem_collect_intv per read
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_smem(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
+                                              const int64_t *offs, const int32_t *sel, int n, Intv *intv_out,
+                                              int32_t *n_intv, uint32_t *status, uint8_t *scratch,
+                                              Counters *ctr)
+{
+    const int nthr = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t nblk = 0;
+    const int vcap = cp.max_len + 2;
+    Intv *sbase = reinterpret_cast<Intv *>(scratch + (size_t)tid * cp.scratch);
+    for (int li = tid; li < n; li += nthr) {
+        const int r = read_of(sel, li);
+        const uint8_t *q = codes + offs[r];
+        const int len = (int)(offs[r + 1] - offs[r]);
+        bool ovf = false;
+        IV mem{intv_out + (size_t)li * cp.intv, 0, cp.intv};
+        IV mem1{sbase, 0, vcap}, va{sbase + vcap, 0, vcap}, vb{sbase + 2 * vcap, 0, vcap};
+        const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
+        int x = 0;
+        // pass 1: SMEMs
+        while (x < len && !ovf) {
+            if (q[x] < 4) {
+                x = smem1(ix, len, q, x, 1, mem1, va, vb, ovf, nblk);
+                for (int i = 0; i < mem1.n && !ovf; ++i) {
+                    const Intv &p = mem1.a[i];
+                    int slen = (int)((uint32_t)p.info - (uint32_t)(p.info >> 32));
+                    if (slen >= o.min_seed_len) mem.push(p, ovf);
+                }
+            } else ++x;
+        }
+        // pass 2: re-seed inside long SMEMs with few occurrences
+        const int old_n = mem.n;
+        for (int k = 0; k < old_n && !ovf; ++k) {
+            Intv p = mem.a[k];
+            int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
+            if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) continue;
+            smem1(ix, len, q, (start + end) >> 1, (int)p.x[2] + 1, mem1, va, vb, ovf, nblk);
+            for (int i = 0; i < mem1.n && !ovf; ++i)
+                if ((uint32_t)mem1.a[i].info - (mem1.a[i].info >> 32) >= (uint64_t)o.min_seed_len) mem.push(mem1.a[i], ovf);
+        }
+        // pass 3: LAST-like seeds
+        if (o.max_mem_intv > 0) {
+            x = 0;
+            while (x < len && !ovf) {
+                if (q[x] < 4) {
+                    Intv m;
+                    x = seed_strategy1(ix, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk);
+                    if (m.x[2] > 0) mem.push(m, ovf);
+                } else ++x;
+            }
+        }
+        if (ovf) {
+            status[li] |= ST_OVERFLOW;
+            n_intv[li] = 0;
+            continue;
+        }
+        // sort by info (equal keys are identical intervals, so any order-correct sort is exact)
+        for (int i = 1; i < mem.n; ++i) {
+            Intv t = mem.a[i];
+            int j = i;
+            while (j > 0 && t.info < mem.a[j - 1].info) { mem.a[j] = mem.a[j - 1]; --j; }
+            mem.a[j] = t;
+        }
+        n_intv[li] = mem.n;
+    }
+    wave_add(&ctr[STG_SMEM].occ_blocks, nblk);
+}
+
+// ------------------------------------------------------------------------------------------------
+// klib ks_introsort (ksort.h) over an index array; lt(x, y) compares element ids.  The pivot,
+// partition and final insertion sort follow klib exactly, so ties land where libbwa puts them.
+// ------------------------------------------------------------------------------------------------
+template <class LT>
+DEV void ks_insertsort(int *a, int n, LT lt)
+{
+    for (int i = 1; i < n; ++i)
+        for (int j = i; j > 0 && lt(a[j], a[j - 1]); --j) { int t = a[j]; a[j] = a[j - 1]; a[j - 1] = t; }
+}
+
+template <class LT>
+DEV void ks_combsort(int *a, int n, LT lt)
+{
+    const double shrink_factor = 1.2473309501039786540366528676643;
+    int do_swap;
+    size_t gap = (size_t)n;
+    do {
+        if (gap > 2) {
+            gap = (size_t)(gap / shrink_factor);
+            if (gap == 9 || gap == 10) gap = 11;
+        }
+        do_swap = 0;
+        for (int i = 0; i < n - (int)gap; ++i) {
+            int j = i + (int)gap;
+            if (lt(a[j], a[i])) { int t = a[i]; a[i] = a[j]; a[j] = t; do_swap = 1; }
+        }
+    } while (do_swap || gap > 2);
+    if (gap != 1) ks_insertsort(a, n, lt);
+}
+
+template <class LT>
+DEV void ks_introsort(int *a, int n, LT lt)
+{
+    if (n < 1) return;
+    if (n == 2) {
+        if (lt(a[1], a[0])) { int t = a[0]; a[0] = a[1]; a[1] = t; }
+        return;
+    }
+    int d;
+    for (d = 2; (1ul << d) < (unsigned long)n; ++d);
+    int stk_l[64], stk_r[64], stk_d[64], top = 0;
+    int s = 0, t = n - 1;
+    d <<= 1;
+    while (1) {
+        if (s < t) {
+            if (--d == 0) {
+                ks_combsort(a + s, t - s + 1, lt);
+                t = s;
+                continue;
+            }
+            int i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            if (lt(a[k], a[i])) {
+                if (lt(a[k], a[j])) k = j;
+            } else k = lt(a[j], a[i]) ? i : j;
+            int rp = a[k];
+            if (k != t) { int x = a[k]; a[k] = a[t]; a[t] = x; }
+            for (;;) {
+                do ++i; while (lt(a[i], rp));
+                do --j; while (i <= j && lt(rp, a[j]));
+                if (j <= i) break;
+                int x = a[i]; a[i] = a[j]; a[j] = x;
+            }
+            { int x = a[i]; a[i] = a[t]; a[t] = x; }
+            if (i - s > t - i) {
+                if (i - s > 16) { stk_l[top] = s; stk_r[top] = i - 1; stk_d[top] = d; ++top; }
+                s = t - i > 16 ? i + 1 : t;
+            } else {
+                if (t - i > 16) { stk_l[top] = i + 1; stk_r[top] = t; stk_d[top] = d; ++top; }
+                t = i - s > 16 ? i - 1 : s;
+            }
+        } else {
+            if (top == 0) { ks_insertsort(a, n, lt); return; }
+            --top; s = stk_l[top]; t = stk_r[top]; d = stk_d[top];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bntseq helpers
+// ------------------------------------------------------------------------------------------------
+DEV int64_t depos(const DIndex &ix, int64_t pos, int &is_rev)
+{
+    return (is_rev = (pos >= ix.l_pac)) ? (ix.l_pac << 1) - 1 - pos : pos;
+}
+
+DEV int pos2rid(const DIndex &ix, int64_t pos_f)
+{
+    if (pos_f >= ix.l_pac) return -1;
+    int left = 0, mid = 0, right = ix.n_anns;
+    while (left < right) {
+        mid = (left + right) >> 1;
+        if (pos_f >= ix.ann_off[mid]) {
+            if (mid == ix.n_anns - 1) break;
+            if (pos_f < ix.ann_off[mid + 1]) break;
+            left = mid + 1;
+        } else right = mid;
+    }
+    return mid;
+}
+
+DEV int intv2rid(const DIndex &ix, int64_t rb, int64_t re)
+{
+    int is_rev;
+    if (rb < ix.l_pac && re > ix.l_pac) return -2;
+    int rid_b = pos2rid(ix, depos(ix, rb, is_rev));
+    int rid_e = rb < re ? pos2rid(ix, depos(ix, re - 1, is_rev)) : rid_b;
+    return rid_b == rid_e ? rid_b : -1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_chain: mem_chain (kbtree t = 5, KB_DEFAULT_SIZE 512) + mem_chain_flt
+// ------------------------------------------------------------------------------------------------
+struct SeedNode { int64_t rbeg; int32_t qbeg, len, next, pad; };
+struct ChainNode { int64_t pos; int32_t rid, n, head, tail, w, kept, first, pad; };
+struct KNode { int32_t n, is_internal; int32_t key[9]; int32_t ptr[10]; };
+#define KB_T 5
+
+struct ChainCtx {
+    SeedNode *seeds; int n_seeds, cap_seeds;
+    ChainNode *ch; int n_ch, cap_ch;
+    KNode *nodes; int n_nodes, cap_nodes;
+    int root, n_keys;
+    bool ovf;
+};
+
+DEV int kb_getp_aux(const ChainCtx &C, const KNode &x, int64_t kpos, int *r)
+{
+    int tr, *rr = r ? r : &tr, begin = 0, end = x.n;
+    if (x.n == 0) return -1;
+    while (begin < end) {
+        int mid = (begin + end) >> 1;
+        if (C.ch[x.key[mid]].pos < kpos) begin = mid + 1;
+        else end = mid;
+    }
+    if (begin == x.n) { *rr = 1; return x.n - 1; }
+    int64_t bp = C.ch[x.key[begin]].pos;
+    if ((*rr = (bp < kpos) - (kpos < bp)) < 0) --begin;
+    return begin;
+}
+
+DEV int kb_intervalp_lower(const ChainCtx &C, int64_t kpos)
+{
+    int i, r = 0, x = C.root, lower = -1;
+    while (x >= 0) {
+        const KNode &nd = C.nodes[x];
+        i = kb_getp_aux(C, nd, kpos, &r);
+        if (i >= 0 && r == 0) return nd.key[i];
+        if (i >= 0) lower = nd.key[i];
+        if (nd.is_internal == 0) return lower;
+        x = nd.ptr[i + 1];
+    }
+    return lower;
+}
+
+DEV int kb_new_node(ChainCtx &C)
+{
+    if (C.n_nodes >= C.cap_nodes) { C.ovf = true; return -1; }
+    KNode &z = C.nodes[C.n_nodes];
+    z.n = 0; z.is_internal = 0;
+    return C.n_nodes++;
+}
+
+DEV bool kb_split(ChainCtx &C, int xi, int i, int yi)
+{
+    int zi = kb_new_node(C);
+    if (zi < 0) return false;
+    KNode &x = C.nodes[xi], &y = C.nodes[yi], &z = C.nodes[zi];
+    z.is_internal = y.is_internal;
+    z.n = KB_T - 1;
+    for (int j = 0; j < KB_T - 1; ++j) z.key[j] = y.key[KB_T + j];
+    if (y.is_internal) for (int j = 0; j < KB_T; ++j) z.ptr[j] = y.ptr[KB_T + j];
+    y.n = KB_T - 1;
+    for (int j = x.n; j >= i + 1; --j) x.ptr[j + 1] = x.ptr[j];
+    x.ptr[i + 1] = zi;
+    for (int j = x.n - 1; j >= i; --j) x.key[j + 1] = x.key[j];
+    x.key[i] = y.key[KB_T - 1];
+    ++x.n;
+    return true;
+}
+
+DEV void kb_putp(ChainCtx &C, int key)
+{
+    ++C.n_keys;
+    int r = C.root;
+    if (C.nodes[r].n == 2 * KB_T - 1) {
+        int s = kb_new_node(C);
+        if (s < 0) return;
+        C.root = s;
+        C.nodes[s].is_internal = 1; C.nodes[s].n = 0;
+        C.nodes[s].ptr[0] = r;
+        if (!kb_split(C, s, 0, r)) return;
+        r = s;
+    }
+    const int64_t kpos = C.ch[key].pos;
+    for (;;) {
+        KNode &x = C.nodes[r];
+        if (x.is_internal == 0) {
+            int i = kb_getp_aux(C, x, kpos, 0);
+            for (int j = x.n - 1; j >= i + 1; --j) x.key[j + 1] = x.key[j];
+            x.key[i + 1] = key;
+            ++x.n;
+            return;
+        }
+        int i = kb_getp_aux(C, x, kpos, 0) + 1;
+        if (C.nodes[x.ptr[i]].n == 2 * KB_T - 1) {
+            if (!kb_split(C, r, i, x.ptr[i])) return;
+            int64_t kp = C.ch[C.nodes[r].key[i]].pos;
+            if (((kp < kpos) - (kpos < kp)) > 0) ++i;
+        }
+        r = C.nodes[r].ptr[i];
+    }
+}
+
+DEV bool test_and_merge(ChainCtx &C, const DOpts &o, int64_t l_pac, int ci, const SeedNode &p, int seed_rid)
+{
+    ChainNode &c = C.ch[ci];
+    const SeedNode &first = C.seeds[c.head], &last = C.seeds[c.tail];
+    int64_t qend = last.qbeg + last.len, rend = last.rbeg + last.len;
+    if (seed_rid != c.rid) return false;
+    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend) return true;
+    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return false;
+    int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
+    if (y >= 0 && x - y <= o.w && y - x <= o.w && x - last.len < o.max_chain_gap && y - last.len < o.max_chain_gap) {
+        if (C.n_seeds >= C.cap_seeds) { C.ovf = true; return true; }
+        int si = C.n_seeds++;
+        C.seeds[si] = p;
+        C.seeds[si].next = -1;
+        C.seeds[c.tail].next = si;
+        c.tail = si;
+        ++c.n;
+        return true;
+    }
+    return false;
+}
+
+DEV int chain_weight(const ChainCtx &C, const ChainNode &c)
+{
+    int64_t end = 0;
+    int w = 0, tmp;
+    for (int s = c.head; s >= 0; s = C.seeds[s].next) {
+        const SeedNode &sd = C.seeds[s];
+        if (sd.qbeg >= end) w += sd.len;
+        else if (sd.qbeg + sd.len > end) w += (int)(sd.qbeg + sd.len - end);
+        end = end > sd.qbeg + sd.len ? end : sd.qbeg + sd.len;
+    }
+    tmp = w; w = 0; end = 0;
+    for (int s = c.head; s >= 0; s = C.seeds[s].next) {
+        const SeedNode &sd = C.seeds[s];
+        if (sd.rbeg >= end) w += sd.len;
+        else if (sd.rbeg + sd.len > end) w += (int)(sd.rbeg + sd.len - end);
+        end = end > sd.rbeg + sd.len ? end : sd.rbeg + sd.len;
+    }
+    w = w < tmp ? w : tmp;
+    return w < (1 << 30) ? w : (1 << 30) - 1;
+}
+
+__global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, const int64_t *offs, const int32_t *sel,
+                                               int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains_out,
+                                               Seed *seeds_out, int32_t *n_chains, uint32_t *status,
+                                               uint8_t *scratch, Counters *ctr)
+{
+    const int nthr = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t nsa = 0;
+    uint8_t *sb = scratch + (size_t)tid * cp.scratch;
+    ChainCtx C;
+    C.seeds = reinterpret_cast<SeedNode *>(sb);
+    C.cap_seeds = cp.seeds;
+    C.ch = reinterpret_cast<ChainNode *>(sb + (size_t)cp.seeds * sizeof(SeedNode));
+    C.cap_ch = cp.chains;
+    C.nodes = reinterpret_cast<KNode *>(sb + (size_t)cp.seeds * sizeof(SeedNode) + (size_t)cp.chains * sizeof(ChainNode));
+    C.cap_nodes = cp.chains / 2 + 8;
+    int *ord = reinterpret_cast<int *>(reinterpret_cast<uint8_t *>(C.nodes) + (size_t)C.cap_nodes * sizeof(KNode));
+    int *kept_list = ord + cp.chains;
+    for (int li = tid; li < n; li += nthr) {
+        n_chains[li] = 0;
+        if (status[li]) continue;
+        const int r = read_of(sel, li);
+        const int len = (int)(offs[r + 1] - offs[r]);
+        if (len < o.min_seed_len) continue;
+        C.n_seeds = 0; C.n_ch = 0; C.n_nodes = 0; C.n_keys = 0; C.ovf = false;
+        C.root = kb_new_node(C);
+        const Intv *mem = intv + (size_t)li * cp.intv;
+        const int nm = n_intv[li];
+        for (int i = 0; i < nm && !C.ovf; ++i) {
+            const Intv p = mem[i];
+            const int slen = (int)((uint32_t)p.info - (uint32_t)(p.info >> 32));
+            const int step = p.x[2] > (uint64_t)o.max_occ ? (int)(p.x[2] / (uint64_t)o.max_occ) : 1;
+            int count = 0;
+            for (int64_t k = 0; (uint64_t)k < p.x[2] && count < o.max_occ && !C.ovf; k += step, ++count) {
+                SeedNode s;
+                s.rbeg = (int64_t)sa_at(ix, p.x[0] + (uint64_t)k);
+                ++nsa;
+                s.qbeg = (int32_t)(p.info >> 32);
+                s.len = slen;
+                s.next = -1;
+                const int rid = intv2rid(ix, s.rbeg, s.rbeg + s.len);
+                if (rid < 0) continue;
+                bool to_add = false;
+                if (C.n_keys) {
+                    int lower = kb_intervalp_lower(C, s.rbeg);
+                    if (lower < 0 || !test_and_merge(C, o, ix.l_pac, lower, s, rid)) to_add = true;
+                } else to_add = true;
+                if (to_add) {
+                    if (C.n_ch >= C.cap_ch || C.n_seeds >= C.cap_seeds) { C.ovf = true; break; }
+                    int si = C.n_seeds++;
+                    C.seeds[si] = s;
+                    int ci = C.n_ch++;
+                    ChainNode &c = C.ch[ci];
+                    c.pos = s.rbeg; c.rid = rid; c.n = 1; c.head = c.tail = si; c.w = 0; c.kept = 0; c.first = -1;
+                    kb_putp(C, ci);
+                }
+            }
+        }
+        if (C.ovf) { status[li] |= ST_OVERFLOW; continue; }
+        // in-order traversal of the B-tree -> chain order
+        int nord = 0;
+        {   // iterative in-order walk == kbtree's __kb_traverse
+            int stn[24], sti[24], std_[24], sp = 0;
+            stn[0] = C.root; sti[0] = 0; std_[0] = 0;
+            while (sp >= 0) {
+                const KNode &nd = C.nodes[stn[sp]];
+                const int i = sti[sp];
+                if (i > nd.n) { --sp; continue; }
+                if (nd.is_internal && !std_[sp]) {      // descend into child i first
+                    std_[sp] = 1;
+                    ++sp; stn[sp] = nd.ptr[i]; sti[sp] = 0; std_[sp] = 0;
+                    continue;
+                }
+                if (i < nd.n) ord[nord++] = nd.key[i];
+                sti[sp] = i + 1; std_[sp] = 0;
+            }
+        }
+        // mem_chain_flt
+        int n_chn = 0;
+        for (int i = 0; i < nord; ++i) {
+            ChainNode &c = C.ch[ord[i]];
+            c.first = -1; c.kept = 0;
+            c.w = chain_weight(C, c);
+            if (c.w >= o.min_chain_weight) ord[n_chn++] = ord[i];
+        }
+        if (n_chn > 0) {
+            ChainNode *ch = C.ch;
+            ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; });
+            ch[ord[0]].kept = 3;
+            int nk = 0;
+            kept_list[nk++] = 0;
+            for (int i = 1; i < n_chn; ++i) {
+                int large_ovlp = 0, k;
+                ChainNode &ci = ch[ord[i]];
+                const int bi = C.seeds[ci.head].qbeg, ei = C.seeds[ci.tail].qbeg + C.seeds[ci.tail].len;
+                for (k = 0; k < nk; ++k) {
+                    int j = kept_list[k];
+                    ChainNode &cj = ch[ord[j]];
+                    const int bj = C.seeds[cj.head].qbeg, ej = C.seeds[cj.tail].qbeg + C.seeds[cj.tail].len;
+                    int b_max = bj > bi ? bj : bi;
+                    int e_min = ej < ei ? ej : ei;
+                    if (e_min > b_max) {   // is_alt is always 0 on this path
+                        int li2 = ei - bi, lj = ej - bj;
+                        int min_l = li2 < lj ? li2 : lj;
+                        if (e_min - b_max >= min_l * o.mask_level && min_l < o.max_chain_gap) {
+                            large_ovlp = 1;
+                            if (cj.first < 0) cj.first = i;
+                            if (ci.w < cj.w * o.drop_ratio && cj.w - ci.w >= o.min_seed_len << 1) break;
+                        }
+                    }
+                }
+                if (k == nk) {
+                    kept_list[nk++] = i;
+                    ci.kept = large_ovlp ? 2 : 3;
+                }
+            }
+            for (int i = 0; i < nk; ++i) {
+                ChainNode &c = ch[ord[kept_list[i]]];
+                if (c.first >= 0) ch[ord[c.first]].kept = 1;
+            }
+            int i, k;
+            for (i = k = 0; i < n_chn; ++i) {
+                if (ch[ord[i]].kept == 0 || ch[ord[i]].kept == 3) continue;
+                if (++k >= o.max_chain_extend) break;
+            }
+            for (; i < n_chn; ++i)
+                if (ch[ord[i]].kept < 3) ch[ord[i]].kept = 0;
+            // write kept chains with contiguous seeds
+            ChainDesc *cd = chains_out + (size_t)li * cp.chains;
+            Seed *so = seeds_out + (size_t)li * cp.seeds;
+            int nc = 0, ns = 0;
+            for (i = 0; i < n_chn; ++i) {
+                const ChainNode &c = ch[ord[i]];
+                if (c.kept == 0) continue;
+                cd[nc].seed_off = ns; cd[nc].n = c.n; cd[nc].rid = c.rid; cd[nc].w = c.w;
+                for (int s = c.head; s >= 0; s = C.seeds[s].next) {
+                    so[ns].rbeg = C.seeds[s].rbeg; so[ns].qbeg = C.seeds[s].qbeg; so[ns].len = C.seeds[s].len;
+                    ++ns;
+                }
+                ++nc;
+            }
+            n_chains[li] = nc;
+        }
+    }
+    wave_add(&ctr[STG_CHAIN].sa_values, nsa);
+}
+
+// ------------------------------------------------------------------------------------------------
+// ksw_extend2 / ksw_global2 (ksw.c) over accessor-defined query and target
+// ------------------------------------------------------------------------------------------------
+struct QAcc {   // query[j] = base[start + dir*j]
+    const uint8_t *base; int start, dir;
+    DEV int operator()(int j) const { return base[start + dir * j]; }
+};
+struct TAcc {   // target[i] = ref_at(start + dir*i)
+    const DIndex *ix; int64_t start; int dir;
+    DEV int operator()(int i) const { return ref_at(*ix, start + (int64_t)dir * i); }
+};
+
+DEV int mat_sc(const DOpts &o, int t, int q)
+{
+    return (t == 4 || q == 4) ? o.mat_amb : (t == q ? o.mat_match : o.mat_mismatch);
+}
+
+DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                     int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
+                     int *_gscore, int *_max_off, int2 *eh, uint64_t &cells)
+{
+    int i, j, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, beg, end, max, max_i, max_j, max_ins, max_del, max_ie,
+        gscore, max_off;
+    if (qlen < 0) qlen = 0;
+    for (j = 0; j <= qlen; ++j) eh[j] = make_int2(0, 0);
+    eh[0].x = h0;
+    if (qlen >= 1) eh[1].x = h0 > oe_ins ? h0 - oe_ins : 0;
+    for (j = 2; j <= qlen && eh[j - 1].x > e_ins; ++j) eh[j].x = eh[j - 1].x - e_ins;
+    max = o.mat_max > 0 ? o.mat_max : 0;
+    max_ins = (int)((double)(qlen * max + end_bonus - o_ins) / e_ins + 1.);
+    max_ins = max_ins > 1 ? max_ins : 1;
+    w = w < max_ins ? w : max_ins;
+    max_del = (int)((double)(qlen * max + end_bonus - o_del) / e_del + 1.);
+    max_del = max_del > 1 ? max_del : 1;
+    w = w < max_del ? w : max_del;
+    max = h0, max_i = max_j = -1; max_ie = -1, gscore = -1;
+    max_off = 0;
+    beg = 0, end = qlen;
+    for (i = 0; i < tlen; ++i) {
+        int t, f = 0, h1, m = 0, mj = -1;
+        const int tb = target(i);
+        if (beg < i - w) beg = i - w;
+        if (end > i + w + 1) end = i + w + 1;
+        if (end > qlen) end = qlen;
+        if (beg == 0) {
+            h1 = h0 - (o_del + e_del * (i + 1));
+            if (h1 < 0) h1 = 0;
+        } else h1 = 0;
+        cells += (uint64_t)(end > beg ? end - beg : 0);
+        for (j = beg; j < end; ++j) {
+            int2 p = eh[j];
+            int h, M = p.x, e = p.y;
+            p.x = h1;
+            M = M ? M + mat_sc(o, tb, query(j)) : 0;
+            h = M > e ? M : e;
+            h = h > f ? h : f;
+            h1 = h;
+            mj = m > h ? mj : j;
+            m = m > h ? m : h;
+            t = M - oe_del; t = t > 0 ? t : 0;
+            e -= e_del; e = e > t ? e : t;
+            p.y = e;
+            eh[j] = p;
+            t = M - oe_ins; t = t > 0 ? t : 0;
+            f -= e_ins; f = f > t ? f : t;
+        }
+        eh[end] = make_int2(h1, 0);
+        if (j == qlen) {
+            max_ie = gscore > h1 ? max_ie : i;
+            gscore = gscore > h1 ? gscore : h1;
+        }
+        if (m == 0) break;
+        if (m > max) {
+            max = m, max_i = i, max_j = mj;
+            int d = mj - i; d = d < 0 ? -d : d;
+            max_off = max_off > d ? max_off : d;
+        } else if (zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (max - m - ((i - max_i) - (mj - max_j)) * e_del > zdrop) break;
+            } else {
+                if (max - m - ((mj - max_j) - (i - max_i)) * e_ins > zdrop) break;
+            }
+        }
+        for (j = beg; j < end && eh[j].x == 0 && eh[j].y == 0; ++j);
+        beg = j;
+        for (j = end; j >= beg && eh[j].x == 0 && eh[j].y == 0; --j);
+        end = j + 2 < qlen ? j + 2 : qlen;
+    }
+    *_qle = max_j + 1;
+    *_tle = max_i + 1;
+    *_gtle = max_ie + 1;
+    *_gscore = gscore;
+    *_max_off = max_off;
+    return max;
+}
+
+#define MINUS_INF (-0x40000000)
+
+// ksw_global2; z == nullptr -> score only.  Returns score; traceback pushed as libbwa push_cigar
+// into cig[] (capacity cap, ops appended then reversed); *ncig = -1 on overflow.
+DEVN int ksw_global2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                     int e_ins, int w, int2 *eh, uint8_t *z, int64_t zcap, uint32_t *cig, int cap, int *ncig,
+                     bool &ovf, uint64_t &cells)
+{
+    int i, j, k, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, score, n_col;
+    n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    if (z && (int64_t)n_col * tlen > zcap) { ovf = true; return 0; }
+    eh[0] = make_int2(0, MINUS_INF);
+    for (j = 1; j <= qlen && j <= w; ++j) eh[j] = make_int2(-(o_ins + e_ins * j), MINUS_INF);
+    for (; j <= qlen; ++j) eh[j] = make_int2(MINUS_INF, MINUS_INF);
+    for (i = 0; i < tlen; ++i) {
+        int32_t f = MINUS_INF, h1, beg, end, t;
+        const int tb = target(i);
+        beg = i > w ? i - w : 0;
+        end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        h1 = beg == 0 ? -(o_del + e_del * (i + 1)) : MINUS_INF;
+        uint8_t *zi = z ? z + (int64_t)i * n_col : nullptr;
+        cells += (uint64_t)(end > beg ? end - beg : 0);
+        for (j = beg; j < end; ++j) {
+            int2 p = eh[j];
+            int32_t h, m = p.x, e = p.y;
+            uint8_t d;
+            p.x = h1;
+            m += mat_sc(o, tb, query(j));
+            d = m >= e ? 0 : 1;
+            h = m >= e ? m : e;
+            d = h >= f ? d : 2;
+            h = h >= f ? h : f;
+            h1 = h;
+            t = m - oe_del;
+            e -= e_del;
+            d |= e > t ? 1 << 2 : 0;
+            e = e > t ? e : t;
+            p.y = e;
+            eh[j] = p;
+            t = m - oe_ins;
+            f -= e_ins;
+            d |= f > t ? 2 << 4 : 0;
+            f = f > t ? f : t;
+            if (zi) zi[j - beg] = d;
+        }
+        eh[end] = make_int2(h1, MINUS_INF);
+    }
+    score = eh[qlen].x;
+    if (z) {
+        int n = 0, which = 0;
+        i = tlen - 1;
+        k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+        auto push = [&](int op, int len) {
+            if (n == 0 || op != (int)(cig[n - 1] & 0xf)) {
+                if (n >= cap) { ovf = true; return; }
+                cig[n++] = (uint32_t)len << 4 | (uint32_t)op;
+            } else cig[n - 1] += (uint32_t)len << 4;
+        };
+        while (i >= 0 && k >= 0 && !ovf) {
+            which = z[(int64_t)i * n_col + (k - (i > w ? i - w : 0))] >> (which << 1) & 3;
+            if (which == 0) push(0, 1), --i, --k;
+            else if (which == 1) push(2, 1), --i;
+            else push(1, 1), --k;
+        }
+        if (i >= 0) push(2, i + 1);
+        if (k >= 0) push(1, k + 1);
+        for (i = 0; i < (n >> 1); ++i) { uint32_t t = cig[i]; cig[i] = cig[n - 1 - i]; cig[n - 1 - i] = t; }
+        *ncig = ovf ? -1 : n;
+    }
+    return score;
+}
+
+// bwa_gen_cigar2 (score + CIGAR; MD/NM are not part of bioseqdb's output)
+DEV int gen_cigar2(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
+                   int64_t re, int *score, int2 *eh, uint8_t *z, int64_t zcap, uint32_t *cig, int cap, int *ncig,
+                   bool &ovf, uint64_t &cells, uint64_t &bases)
+{
+    *ncig = 0;
+    if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
+    int64_t rlen = re - rb;   // bns_get_seq never clamps here: [rb,re) lies inside [0, 2*l_pac)
+    if (re > (ix.l_pac << 1) || rb < 0) return 0;
+    bases += (uint64_t)((rlen + 3) >> 2);
+    const bool rev = rb >= ix.l_pac;
+    QAcc qa{q, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
+    TAcc ta{&ix, rev ? re - 1 : rb, rev ? -1 : 1};
+    if (l_query == rlen && w_ == 0) {
+        if (z) {
+            if (cap < 1) { ovf = true; return 0; }
+            cig[0] = (uint32_t)l_query << 4;
+            *ncig = 1;
+        }
+        int s = 0;
+        for (int i = 0; i < l_query; ++i) s += mat_sc(o, ta(i), qa(i));
+        *score = s;
+    } else {
+        int w, max_gap, max_ins, max_del, min_w;
+        max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
+        max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+        max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
+        w = (max_gap + dl + 1) >> 1;
+        w = w < w_ ? w : w_;
+        min_w = dl + 3;
+        w = w > min_w ? w : min_w;
+        *score = ksw_global2(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, z, zcap, cig,
+                             cap, ncig, ovf, cells);
+    }
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_extend: mem_chain2aln for every chain, mem_sort_dedup_patch, mem_mark_primary_se
+// ------------------------------------------------------------------------------------------------
+DEV int cal_max_gap(const DOpts &o, int qlen)
+{
+    int l_del = (int)((double)(qlen * o.a - o.o_del) / o.e_del + 1.);
+    int l_ins = (int)((double)(qlen * o.a - o.o_ins) / o.e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < o.w << 1 ? l : o.w << 1;
+}
+
+DEV uint64_t hash_64(uint64_t key)
+{
+    key += ~(key << 32);
+    key ^= (key >> 22);
+    key += ~(key << 13);
+    key ^= (key >> 8);
+    key += (key << 3);
+    key ^= (key >> 15);
+    key += ~(key << 27);
+    key ^= (key >> 31);
+    return key;
+}
+
+struct ExtCtx {
+    Reg *av; int n, cap;
+    Reg *tmp;
+    int *idx;
+    uint64_t *srt;
+    int2 *eh;
+    bool ovf;
+};
+
+DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
+                   ExtCtx &X, uint64_t &cells, uint64_t &bases)
+{
+    int64_t l_pac = ix.l_pac, rmax0, rmax1;
+    if (c.n == 0) return;
+    rmax0 = l_pac << 1; rmax1 = 0;
+    for (int i = 0; i < c.n; ++i) {
+        const Seed &t = seeds[i];
+        int64_t b = t.rbeg - (t.qbeg + cal_max_gap(o, t.qbeg));
+        int64_t e = t.rbeg + t.len + ((l_query - t.qbeg - t.len) + cal_max_gap(o, l_query - t.qbeg - t.len));
+        rmax0 = rmax0 < b ? rmax0 : b;
+        rmax1 = rmax1 > e ? rmax1 : e;
+    }
+    rmax0 = rmax0 > 0 ? rmax0 : 0;
+    rmax1 = rmax1 < l_pac << 1 ? rmax1 : l_pac << 1;
+    if (rmax0 < l_pac && l_pac < rmax1) {
+        if (seeds[0].rbeg < l_pac) rmax1 = l_pac;
+        else rmax0 = l_pac;
+    }
+    {   // bns_fetch_seq: clamp to the row (strand-flipped) containing seeds[0]
+        int is_rev;
+        int rid = pos2rid(ix, depos(ix, seeds[0].rbeg, is_rev));
+        int64_t far_beg = ix.ann_off[rid], far_end = far_beg + ix.ann_len[rid];
+        if (is_rev) { int64_t t = far_beg; far_beg = (l_pac << 1) - far_end; far_end = (l_pac << 1) - t; }
+        rmax0 = rmax0 > far_beg ? rmax0 : far_beg;
+        rmax1 = rmax1 < far_end ? rmax1 : far_end;
+        bases += (uint64_t)((rmax1 - rmax0 + 3) >> 2);
+    }
+    uint64_t *srt = X.srt;
+    for (int i = 0; i < c.n; ++i) srt[i] = (uint64_t)(uint32_t)seeds[i].len << 32 | (uint64_t)i;   // score == len
+    for (int i = 1; i < c.n; ++i) {   // keys are unique: any correct sort equals ks_introsort_64
+        uint64_t t = srt[i];
+        int j = i;
+        while (j > 0 && t < srt[j - 1]) { srt[j] = srt[j - 1]; --j; }
+        srt[j] = t;
+    }
+    for (int k = c.n - 1; k >= 0; --k) {
+        const Seed s = seeds[(uint32_t)srt[k]];
+        int i;
+        for (i = 0; i < X.n; ++i) {
+            const Reg &p = X.av[i];
+            if (s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) continue;
+            if (s.len - p.seedlen0 > .1 * l_query) continue;
+            int qd = s.qbeg - p.qb;
+            int64_t rd = s.rbeg - p.rb;
+            int max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
+            int w = max_gap < p.w ? max_gap : p.w;
+            if (qd - rd < w && rd - qd < w) break;
+            qd = p.qe - (s.qbeg + s.len);
+            rd = p.re - (s.rbeg + s.len);
+            max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
+            w = max_gap < p.w ? max_gap : p.w;
+            if (qd - rd < w && rd - qd < w) break;
+        }
+        if (i < X.n) {
+            for (i = k + 1; i < c.n; ++i) {
+                if (srt[i] == 0) continue;
+                const Seed &t = seeds[(uint32_t)srt[i]];
+                if (t.len < s.len * .95) continue;
+                if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && t.qbeg - s.qbeg != t.rbeg - s.rbeg) break;
+                if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && s.qbeg - t.qbeg != s.rbeg - t.rbeg) break;
+            }
+            if (i == c.n) { srt[k] = 0; continue; }
+        }
+        if (X.n >= X.cap) { X.ovf = true; return; }
+        Reg &a = X.av[X.n++];
+        a = Reg{};
+        int aw0, aw1, max_off0 = 0, max_off1 = 0;
+        a.w = aw0 = aw1 = o.w;
+        a.score = a.truesc = -1;
+        a.rid = c.rid;
+        if (s.qbeg) {
+            int qle, tle, gtle, gscore;
+            int64_t tmp = s.rbeg - rmax0;
+            QAcc qa{q, s.qbeg - 1, -1};
+            TAcc ta{&ix, s.rbeg - 1, -1};
+            for (int t = 0; t < 2; ++t) {
+                int prev = a.score;
+                aw0 = o.w << t;
+                a.score = ksw_extend2(o, s.qbeg, qa, (int)tmp, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, aw0, o.pen_clip5,
+                                      o.zdrop, s.len * o.a, &qle, &tle, &gtle, &gscore, &max_off0, X.eh, cells);
+                if (a.score == prev || max_off0 < (aw0 >> 1) + (aw0 >> 2)) break;
+            }
+            if (gscore <= 0 || gscore <= a.score - o.pen_clip5) {
+                a.qb = s.qbeg - qle, a.rb = s.rbeg - tle;
+                a.truesc = a.score;
+            } else {
+                a.qb = 0, a.rb = s.rbeg - gtle;
+                a.truesc = gscore;
+            }
+        } else a.score = a.truesc = s.len * o.a, a.qb = 0, a.rb = s.rbeg;
+        if (s.qbeg + s.len != l_query) {
+            int qle, tle, gtle, gscore, sc0 = a.score;
+            int qe = s.qbeg + s.len;
+            int re = (int)(s.rbeg + s.len - rmax0);
+            QAcc qa{q, qe, 1};
+            TAcc ta{&ix, rmax0 + re, 1};
+            for (int t = 0; t < 2; ++t) {
+                int prev = a.score;
+                aw1 = o.w << t;
+                a.score = ksw_extend2(o, l_query - qe, qa, (int)(rmax1 - rmax0 - re), ta, o.o_del, o.e_del, o.o_ins,
+                                      o.e_ins, aw1, o.pen_clip3, o.zdrop, sc0, &qle, &tle, &gtle, &gscore, &max_off1,
+                                      X.eh, cells);
+                if (a.score == prev || max_off1 < (aw1 >> 1) + (aw1 >> 2)) break;
+            }
+            if (gscore <= 0 || gscore <= a.score - o.pen_clip3) {
+                a.qe = qe + qle, a.re = rmax0 + re + tle;
+                a.truesc += a.score - sc0;
+            } else {
+                a.qe = l_query, a.re = rmax0 + re + gtle;
+                a.truesc += gscore - sc0;
+            }
+        } else a.qe = l_query, a.re = s.rbeg + s.len;
+        a.seedcov = 0;
+        for (int i2 = 0; i2 < c.n; ++i2) {
+            const Seed &t = seeds[i2];
+            if (t.qbeg >= a.qb && t.qbeg + t.len <= a.qe && t.rbeg >= a.rb && t.rbeg + t.len <= a.re) a.seedcov += t.len;
+        }
+        a.w = aw0 > aw1 ? aw0 : aw1;
+        a.seedlen0 = s.len;
+    }
+}
+
+DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg &a, const Reg &b, int *_w, int2 *eh,
+                  uint64_t &cells, uint64_t &bases)
+{
+    int w, score = 0, q_s, r_s;
+    double r;
+    if (a.rb < ix.l_pac && b.rb >= ix.l_pac) return 0;
+    if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) return 0;
+    w = (int)((a.re - b.rb) - (a.qe - b.qb));
+    w = w > 0 ? w : -w;
+    r = (double)(a.re - b.rb) / (b.re - a.rb) - (double)(a.qe - b.qb) / (b.qe - a.qb);
+    r = r > 0. ? r : -r;
+    if (a.re < b.rb || a.qe < b.qb) {
+        if (w > o.w << 1 || r >= 0.05f) return 0;
+    } else if (w > o.w << 2 || r >= 0.05f * 2) return 0;
+    w += a.w + b.w;
+    w = w < o.w << 2 ? w : o.w << 2;
+    int ncig = 0;
+    bool dummy = false;
+    gen_cigar2(ix, o, w, q, a.qb, b.qe - a.qb, a.rb, b.re, &score, eh, nullptr, 0, nullptr, 0, &ncig, dummy, cells, bases);
+    q_s = (int)((double)(b.qe - a.qb) / ((b.qe - b.qb) + (a.qe - a.qb)) * (b.score + a.score) + .499);
+    r_s = (int)((double)(b.re - a.rb) / ((b.re - b.rb) + (a.re - a.rb)) * (b.score + a.score) + .499);
+    if ((double)score / (q_s > r_s ? q_s : r_s) < 0.90f) return 0;
+    *_w = w;
+    return score;
+}
+
+DEV void permute(ExtCtx &X, int n)
+{
+    for (int i = 0; i < n; ++i) X.tmp[i] = X.av[X.idx[i]];
+    for (int i = 0; i < n; ++i) X.av[i] = X.tmp[i];
+}
+
+DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, ExtCtx &X, uint64_t &cells, uint64_t &bases)
+{
+    int n = X.n, m, i, j;
+    if (n <= 1) return n;
+    Reg *a = X.av;
+    for (i = 0; i < n; ++i) X.idx[i] = i;
+    ks_introsort(X.idx, n, [a](int x, int y) { return a[x].re < a[y].re; });
+    permute(X, n);
+    for (i = 0; i < n; ++i) a[i].n_comp = 1;
+    for (i = 1; i < n; ++i) {
+        Reg *p = &a[i];
+        if (p->rid != a[i - 1].rid || p->rb >= a[i - 1].re + o.max_chain_gap) continue;
+        for (j = i - 1; j >= 0 && p->rid == a[j].rid && p->rb < a[j].re + o.max_chain_gap; --j) {
+            Reg *qq = &a[j];
+            int64_t or_, oq, mr, mq;
+            int score, w;
+            if (qq->qe == qq->qb) continue;
+            or_ = qq->re - p->rb;
+            oq = qq->qb < p->qb ? qq->qe - p->qb : p->qe - qq->qb;
+            mr = qq->re - qq->rb < p->re - p->rb ? qq->re - qq->rb : p->re - p->rb;
+            mq = qq->qe - qq->qb < p->qe - p->qb ? qq->qe - qq->qb : p->qe - p->qb;
+            if (or_ > o.mask_level_redun * mr && oq > o.mask_level_redun * mq) {
+                if (p->score < qq->score) { p->qe = p->qb; break; }
+                else qq->qe = qq->qb;
+            } else if (qq->rb < p->rb && (score = patch_reg(ix, o, q, *qq, *p, &w, X.eh, cells, bases)) > 0) {
+                p->n_comp += qq->n_comp + 1;
+                p->seedcov = p->seedcov > qq->seedcov ? p->seedcov : qq->seedcov;
+                p->sub = p->sub > qq->sub ? p->sub : qq->sub;
+                p->csub = p->csub > qq->csub ? p->csub : qq->csub;
+                p->qb = qq->qb, p->rb = qq->rb;
+                p->truesc = p->score = score;
+                p->w = w;
+                qq->qb = qq->qe;
+            }
+        }
+    }
+    for (i = 0, m = 0; i < n; ++i)
+        if (a[i].qe > a[i].qb) { if (m != i) a[m++] = a[i]; else ++m; }
+    n = m;
+    for (i = 0; i < n; ++i) X.idx[i] = i;
+    ks_introsort(X.idx, n, [a](int x, int y) {
+        return a[x].score > a[y].score || (a[x].score == a[y].score && (a[x].rb < a[y].rb || (a[x].rb == a[y].rb && a[x].qb < a[y].qb)));
+    });
+    permute(X, n);
+    for (i = 1; i < n; ++i)
+        if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
+    for (i = 1, m = 1; i < n; ++i)
+        if (a[i].qe > a[i].qb) { if (m != i) a[m++] = a[i]; else ++m; }
+    return m;
+}
+
+DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
+{
+    int n = X.n;
+    if (n == 0) return;
+    Reg *a = X.av;
+    for (int i = 0; i < n; ++i) {
+        a[i].sub = 0; a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i));
+        X.idx[i] = i;
+    }
+    ks_introsort(X.idx, n, [a](int x, int y) {
+        return a[x].score > a[y].score || (a[x].score == a[y].score && a[x].hash < a[y].hash);
+    });
+    permute(X, n);
+    int tmp = o.a + o.b;
+    tmp = o.o_del + o.e_del > tmp ? o.o_del + o.e_del : tmp;
+    tmp = o.o_ins + o.e_ins > tmp ? o.o_ins + o.e_ins : tmp;
+    int *z = X.idx, nz = 0;
+    z[nz++] = 0;
+    for (int i = 1; i < n; ++i) {
+        int k;
+        for (k = 0; k < nz; ++k) {
+            int j = z[k];
+            int b_max = a[j].qb > a[i].qb ? a[j].qb : a[i].qb;
+            int e_min = a[j].qe < a[i].qe ? a[j].qe : a[i].qe;
+            if (e_min > b_max) {
+                int min_l = a[i].qe - a[i].qb < a[j].qe - a[j].qb ? a[i].qe - a[i].qb : a[j].qe - a[j].qb;
+                if (e_min - b_max >= min_l * o.mask_level) {
+                    if (a[j].sub == 0) a[j].sub = a[i].score;
+                    if (a[j].score - a[i].score <= tmp) ++a[j].sub_n;
+                    break;
+                }
+            }
+        }
+        if (k == nz) z[nz++] = i;
+        else a[i].secondary = z[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_extend(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+                                                const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
+                                                const Seed *seeds, const int32_t *n_chains, Reg *regs_out,
+                                                int32_t *n_regs, uint32_t *status, uint8_t *scratch, Counters *ctr)
+{
+    const int nthr = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t cells = 0, bases = 0;
+    uint8_t *sb = scratch + (size_t)tid * cp.scratch;
+    ExtCtx X;
+    X.tmp = reinterpret_cast<Reg *>(sb);
+    X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
+    X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
+    X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
+    for (int li = tid; li < n; li += nthr) {
+        n_regs[li] = 0;
+        if (status[li]) continue;
+        const int r = read_of(sel, li);
+        const uint8_t *q = codes + offs[r];
+        const int len = (int)(offs[r + 1] - offs[r]);
+        X.av = regs_out + (size_t)li * cp.regs;
+        X.n = 0; X.cap = cp.regs; X.ovf = false;
+        const ChainDesc *cd = chains + (size_t)li * cp.chains;
+        const Seed *sd = seeds + (size_t)li * cp.seeds;
+        const int nc = n_chains[li];
+        for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, cells, bases);
+        if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
+        X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
+        mark_primary_se(o, X, ids[r]);
+        n_regs[li] = X.n;
+    }
+    wave_add(&ctr[STG_EXTEND].dp_cells, cells);
+    wave_add(&ctr[STG_EXTEND].ref_bases, bases);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_reg2aln: mem_reg2aln per region
+// ------------------------------------------------------------------------------------------------
+DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
+{
+    int w;
+    if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
+    w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
+    int d = l1 - l2; d = d < 0 ? -d : d;
+    if (w < d) w = d;
+    return w;
+}
+
+__global__ void __launch_bounds__(256) k_reg2aln(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+                                                 const int32_t *sel, int n, const Reg *regs, const int32_t *n_regs,
+                                                 Hit *hits, uint32_t *cigars, int32_t *n_cig_read, uint32_t *status,
+                                                 uint8_t *scratch, Counters *ctr)
+{
+    const int nthr = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t cells = 0, bases = 0;
+    uint8_t *sb = scratch + (size_t)tid * cp.scratch;
+    int2 *eh = reinterpret_cast<int2 *>(sb);
+    const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 63) & ~(size_t)63;
+    uint8_t *z = sb + eh_bytes;
+    const int64_t zcap = cp.scratch - (int64_t)eh_bytes;
+    for (int li = tid; li < n; li += nthr) {
+        n_cig_read[li] = 0;
+        if (status[li]) continue;
+        const int r = read_of(sel, li);
+        const uint8_t *q = codes + offs[r];
+        const int l_query = (int)(offs[r + 1] - offs[r]);
+        const int nr = n_regs[li];
+        bool ovf = false;
+        int tot = 0;
+        for (int g = 0; g < nr && !ovf; ++g) {
+            const Reg &ar = regs[(size_t)li * cp.regs + g];
+            Hit &h = hits[(size_t)li * cp.regs + g];
+            uint32_t *cig = cigars + ((size_t)li * cp.regs + g) * cp.cigar;
+            const int qb = ar.qb, qe = ar.qe;
+            const int64_t rb = ar.rb, re = ar.re;
+            int flag = ar.secondary >= 0 ? 0x100 : 0;
+            int tmp = infer_bw(qe - qb, (int)(re - rb), ar.truesc, o.a, o.o_del, o.e_del);
+            int w2 = infer_bw(qe - qb, (int)(re - rb), ar.truesc, o.a, o.o_ins, o.e_ins);
+            w2 = w2 > tmp ? w2 : tmp;
+            if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
+            int i = 0, score = 0, last_sc = -(1 << 30), ncig = 0;
+            do {
+                w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+                gen_cigar2(ix, o, w2, q, qb, qe - qb, rb, re, &score, eh, z, zcap, cig, cp.cigar - 2, &ncig, ovf, cells, bases);
+                if (ovf) break;
+                if (score == last_sc || w2 == o.w << 2) break;
+                last_sc = score;
+                w2 <<= 1;
+            } while (++i < 3 && score < ar.truesc - o.a);
+            if (ovf) break;
+            int is_rev;
+            int64_t pos = depos(ix, rb < ix.l_pac ? rb : re - 1, is_rev);
+            (void)pos;
+            if (ncig > 0) {
+                if ((cig[0] & 0xf) == 2) {
+                    --ncig;
+                    for (int t = 0; t < ncig; ++t) cig[t] = cig[t + 1];
+                } else if ((cig[ncig - 1] & 0xf) == 2) --ncig;
+            }
+            if (qb != 0 || qe != l_query) {
+                int clip5 = is_rev ? l_query - qe : qb, clip3 = is_rev ? qb : l_query - qe;
+                if (clip5) {
+                    for (int t = ncig; t > 0; --t) cig[t] = cig[t - 1];
+                    cig[0] = (uint32_t)clip5 << 4 | 3;
+                    ++ncig;
+                }
+                if (clip3) cig[ncig++] = (uint32_t)clip3 << 4 | 3;
+            }
+            h.rb = rb; h.re = re; h.qb = qb; h.qe = qe; h.rid = ar.rid; h.score = ar.score; h.flag = flag;
+            h.is_rev = is_rev; h.n_cigar = ncig; h.pad = 0;
+            tot += ncig;
+        }
+        if (ovf) { status[li] |= ST_OVERFLOW; continue; }
+        n_cig_read[li] = tot;
+    }
+    wave_add(&ctr[STG_REG2ALN].dp_cells, cells);
+    wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
+}
+
+// ------------------------------------------------------------------------------------------------
+// packing: per-read counts from the main or the retry workspace, then scatter into bsq_hits
+// ------------------------------------------------------------------------------------------------
+struct SlotView {
+    const Hit *hits; const uint32_t *cigars; const int32_t *n_regs; const int32_t *n_cig; Caps cp;
+};
+
+__global__ void k_counts(int n, SlotView mv, SlotView rv, const int32_t *retry_slot, const uint32_t *status,
+                         int64_t *cnt_hits, int64_t *cnt_cig, unsigned long long *unresolved)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int rs = retry_slot ? retry_slot[i] : -1;
+    if (rs >= 0) {
+        cnt_hits[i] = rv.n_regs[rs];
+        cnt_cig[i] = rv.n_cig[rs];
+    } else {
+        if (status[i]) atomicAdd(unresolved, 1ull);
+        cnt_hits[i] = status[i] ? 0 : mv.n_regs[i];
+        cnt_cig[i] = status[i] ? 0 : mv.n_cig[i];
+    }
+}
+
+__global__ void k_pack(int n, SlotView mv, SlotView rv, const int32_t *retry_slot, const int64_t *off_hits,
+                       const int64_t *off_cig, const int64_t *ann_off, const int64_t *ann_id, bsq_hit *out,
+                       uint32_t *out_cig)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int rs = retry_slot ? retry_slot[i] : -1;
+    const SlotView &v = rs >= 0 ? rv : mv;
+    const int slot = rs >= 0 ? rs : i;
+    const int nh = rs >= 0 ? rv.n_regs[rs] : (int)(off_hits[i + 1] - off_hits[i]);
+    int64_t oc = off_cig[i];
+    for (int g = 0; g < nh; ++g) {
+        const Hit &h = v.hits[(size_t)slot * v.cp.regs + g];
+        bsq_hit &b = out[off_hits[i] + g];
+        const int64_t roff = ann_off[h.rid];
+        b.ref_id = ann_id[h.rid];
+        b.rb = h.rb; b.re = h.re;
+        b.ref_match_start = (int32_t)(h.rb - roff);
+        b.ref_match_end = (int32_t)(h.re - roff);
+        b.ref_match_len = (int32_t)(h.re - h.rb);
+        b.qb = h.qb; b.qe = h.qe; b.score = h.score; b.rid = h.rid;
+        b.is_primary = (h.flag & 0x100) == 0; b.is_secondary = (h.flag & 0x100) != 0; b.is_reverse = h.is_rev != 0;
+        b.pad0 = 0;
+        b.read_index = i;
+        b.cigar_off = (uint32_t)oc; b.n_cigar = (uint32_t)h.n_cigar;
+        const uint32_t *src = v.cigars + ((size_t)slot * v.cp.regs + g) * v.cp.cigar;
+        for (int t = 0; t < h.n_cigar; ++t) out_cig[oc + t] = src[t];
+        oc += h.n_cigar;
+    }
+}
+
+__global__ void k_collect_overflow(int n, const uint32_t *status, int32_t *list, int32_t *count)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (status[i] & ST_OVERFLOW) {
+        int k = atomicAdd(count, 1);
+        list[k] = i;
+    }
+}
+
+}  // namespace bsq
+
+// ------------------------------------------------------------------------------------------------
+// host-side launchers (called from bsq_api.cpp)
+// ------------------------------------------------------------------------------------------------
+namespace bsq {
+
+hipError_t launch_smem(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                       const int64_t *offs, const int32_t *sel, int n, Intv *intv, int32_t *n_intv, uint32_t *status,
+                       uint8_t *scratch, Counters *ctr)
+{
+    hipLaunchKernelGGL(k_smem, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, n, intv, n_intv, status, scratch, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const int64_t *offs,
+                        const int32_t *sel, int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains,
+                        Seed *seeds, int32_t *n_chains, uint32_t *status, uint8_t *scratch, Counters *ctr)
+{
+    hipLaunchKernelGGL(k_chain, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds, n_chains,
+                       status, scratch, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                         const int64_t *offs, const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
+                         const Seed *seeds, const int32_t *n_chains, Reg *regs, int32_t *n_regs, uint32_t *status,
+                         uint8_t *scratch, Counters *ctr)
+{
+    hipLaunchKernelGGL(k_extend, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds, n_chains,
+                       regs, n_regs, status, scratch, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_reg2aln(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                          const int64_t *offs, const int32_t *sel, int n, const Reg *regs, const int32_t *n_regs,
+                          Hit *hits, uint32_t *cigars, int32_t *n_cig, uint32_t *status, uint8_t *scratch, Counters *ctr)
+{
+    hipLaunchKernelGGL(k_reg2aln, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, n, regs, n_regs, hits, cigars,
+                       n_cig, status, scratch, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_counts(hipStream_t st, int n, const SlotView &mv, const SlotView &rv, const int32_t *retry_slot,
+                         const uint32_t *status, int64_t *cnt_hits, int64_t *cnt_cig, unsigned long long *unresolved)
+{
+    hipLaunchKernelGGL(k_counts, dim3((n + 255) / 256), dim3(256), 0, st, n, mv, rv, retry_slot, status, cnt_hits, cnt_cig,
+                       unresolved);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(hipStream_t st, int n, const SlotView &mv, const SlotView &rv, const int32_t *retry_slot,
+                       const int64_t *off_hits, const int64_t *off_cig, const int64_t *ann_off, const int64_t *ann_id,
+                       bsq_hit *out, uint32_t *out_cig)
+{
+    hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, st, n, mv, rv, retry_slot, off_hits, off_cig, ann_off,
+                       ann_id, out, out_cig);
+    return hipGetLastError();
+}
+
+hipError_t launch_collect_overflow(hipStream_t st, int n, const uint32_t *status, int32_t *list, int32_t *count)
+{
+    hipLaunchKernelGGL(k_collect_overflow, dim3((n + 255) / 256), dim3(256), 0, st, n, status, list, count);
+    return hipGetLastError();
+}
+
+}  // namespace bsq

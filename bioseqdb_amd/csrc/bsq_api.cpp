@@ -1,0 +1,741 @@
+// bsq_api.cpp -- C-ABI implementation (include/bsq.h): index lifecycle, HBM upload, batch workspace
+// management, kernel orchestration on a per-batch HIP stream, overflow retry, result packing.
+//
+// Host-side orchestration of the path that bioseqdb runs as BwaIndex::align_sequence per cursor row
+// (bioseqdb/bwa.cpp:190-230, bioseqdb/extension.cpp:362-370).  There is no CPU fallback: every
+// alignment result comes from the HIP kernels in align_kernels.hip; without a device the calls fail
+// with BSQ_E_NODEV.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/bsq.h"
+#include "bsq_device.h"
+#include "bsq_index.h"
+
+namespace bsq {
+hipError_t launch_smem(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                       const int32_t *, int, Intv *, int32_t *, uint32_t *, uint8_t *, Counters *);
+hipError_t launch_chain(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const int64_t *, const int32_t *,
+                        int, const Intv *, const int32_t *, ChainDesc *, Seed *, int32_t *, uint32_t *, uint8_t *,
+                        Counters *);
+hipError_t launch_extend(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                         const int32_t *, const int64_t *, int, const ChainDesc *, const Seed *, const int32_t *, Reg *,
+                         int32_t *, uint32_t *, uint8_t *, Counters *);
+hipError_t launch_reg2aln(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                          const int32_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *, uint32_t *,
+                          uint8_t *, Counters *);
+struct SlotView { const Hit *hits; const uint32_t *cigars; const int32_t *n_regs; const int32_t *n_cig; Caps cp; };
+hipError_t launch_counts(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const uint32_t *, int64_t *,
+                         int64_t *, unsigned long long *);
+hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const int64_t *,
+                       const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *);
+hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
+}  // namespace bsq
+
+using namespace bsq;
+
+static thread_local std::string g_err;
+static void set_err(const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__);       \
+            return BSQ_E_HIP;                                                                      \
+        }                                                                                          \
+    } while (0)
+
+extern "C" const char *bsq_last_error(void) { return g_err.c_str(); }
+extern "C" const char *bsq_version(void) { return "bsq 0.1 (gfx950)"; }
+extern "C" void bsq_free(void *p) { free(p); }
+
+extern "C" int bsq_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int default_threads()
+{
+    const char *e = getenv("BSQ_THREADS");
+    if (!e) e = getenv("OMP_NUM_THREADS");
+    int t = e ? atoi(e) : 0;
+    if (t <= 0) {
+        t = (int)std::thread::hardware_concurrency();
+        if (t > 16) t = 16;
+    }
+    return t < 1 ? 1 : t;
+}
+
+// ================================================================================================
+// index
+// ================================================================================================
+namespace bsq {
+struct DeviceIndex {
+    int device = -1;
+    OccBlock *occ = nullptr;
+    void *sa = nullptr;
+    uint8_t *pac = nullptr;
+    int64_t *ann_off = nullptr, *ann_id = nullptr;
+    int32_t *ann_len = nullptr;
+    DIndex view{};
+    ~DeviceIndex()
+    {
+        if (device >= 0) hipSetDevice(device);
+        hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len);
+    }
+};
+}  // namespace bsq
+
+
+extern "C" int bsq_index_create(bsq_index **out)
+{
+    if (!out) { set_err("null out"); return BSQ_E_INVALID; }
+    *out = new (std::nothrow) bsq_index();
+    if (!*out) { set_err("out of memory"); return BSQ_E_NOMEM; }
+    return BSQ_OK;
+}
+
+extern "C" void bsq_index_free(bsq_index *idx)
+{
+    if (!idx) return;
+    delete idx->h.dev;
+    delete idx;
+}
+
+extern "C" int bsq_index_add_ref(bsq_index *idx, int64_t id, const void *nuclseq)
+{
+    if (!idx || !nuclseq) { set_err("null argument"); return BSQ_E_INVALID; }
+    if (idx->h.dev) { set_err("index already uploaded; references are immutable"); return BSQ_E_INVALID; }
+    idx->h.add_ref(id, static_cast<const uint8_t *>(nuclseq));
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_build(bsq_index *idx, int threads)
+{
+    if (!idx) { set_err("null index"); return BSQ_E_INVALID; }
+    std::string err;
+    try {
+        if (idx->h.build(threads > 0 ? threads : default_threads(), err) != 0) {
+            set_err("index build failed: %s", err.c_str());
+            return BSQ_E_INVALID;
+        }
+    } catch (const std::bad_alloc &) {
+        set_err("out of host memory building the index");
+        return BSQ_E_NOMEM;
+    }
+    return BSQ_OK;
+}
+
+extern "C" int64_t bsq_index_l_pac(const bsq_index *idx) { return idx ? idx->h.l_pac : -1; }
+extern "C" int64_t bsq_index_seq_len(const bsq_index *idx) { return idx ? (int64_t)idx->h.seq_len : -1; }
+extern "C" int64_t bsq_index_primary(const bsq_index *idx) { return idx ? (int64_t)idx->h.primary : -1; }
+extern "C" int32_t bsq_index_n_refs(const bsq_index *idx) { return idx ? (int32_t)idx->h.anns.size() : -1; }
+
+extern "C" int64_t bsq_index_sa(const bsq_index *idx, int64_t row)
+{
+    if (!idx || !idx->h.built || row < 0 || (uint64_t)row > idx->h.seq_len || idx->h.seq_len == 0) return -1;
+    return (int64_t)idx->h.sa((uint64_t)row);
+}
+
+extern "C" int bsq_index_occ4(const bsq_index *idx, int64_t k, uint64_t cnt[4])
+{
+    if (!idx || !idx->h.built || idx->h.seq_len == 0) { set_err("index not built"); return BSQ_E_INVALID; }
+    if (k < -1 || (uint64_t)k > idx->h.seq_len) { set_err("row out of range"); return BSQ_E_INVALID; }
+    idx->h.occ4((uint64_t)k, cnt);
+    return BSQ_OK;
+}
+
+extern "C" const void *bsq_index_sa_data(const bsq_index *idx, int *elem_bytes)
+{
+    if (!idx || !idx->h.built || idx->h.seq_len == 0) return nullptr;
+    if (!idx->h.sa32.empty()) { if (elem_bytes) *elem_bytes = 4; return idx->h.sa32.data(); }
+    if (elem_bytes) *elem_bytes = 8;
+    return idx->h.sa64.data();
+}
+
+extern "C" int bsq_index_upload(bsq_index *idx, int device)
+{
+    if (!idx || !idx->h.built) { set_err("index not built"); return BSQ_E_INVALID; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+        set_err("no HIP device %d (found %d); the alignment path has no CPU fallback", device, ndev);
+        return BSQ_E_NODEV;
+    }
+    HIPCHK(hipSetDevice(device));
+    delete idx->h.dev;
+    idx->h.dev = new DeviceIndex();
+    DeviceIndex *d = idx->h.dev;
+    d->device = device;
+    const HostIndex &h = idx->h;
+    const size_t nann = h.anns.size() ? h.anns.size() : 1;
+    std::vector<int64_t> off(nann, 0), id(nann, 0);
+    std::vector<int32_t> len(nann, 0);
+    for (size_t i = 0; i < h.anns.size(); ++i) { off[i] = h.anns[i].offset; id[i] = h.anns[i].id; len[i] = h.anns[i].len; }
+    HIPCHK(hipMalloc(&d->ann_off, nann * 8));
+    HIPCHK(hipMalloc(&d->ann_id, nann * 8));
+    HIPCHK(hipMalloc(&d->ann_len, nann * 4));
+    HIPCHK(hipMemcpy(d->ann_off, off.data(), nann * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->ann_id, id.data(), nann * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->ann_len, len.data(), nann * 4, hipMemcpyHostToDevice));
+    if (h.seq_len > 0) {
+        HIPCHK(hipMalloc(&d->occ, h.occ.size() * sizeof(OccBlock)));
+        HIPCHK(hipMemcpy(d->occ, h.occ.data(), h.occ.size() * sizeof(OccBlock), hipMemcpyHostToDevice));
+        size_t sab = h.sa32.empty() ? h.sa64.size() * 8 : h.sa32.size() * 4;
+        HIPCHK(hipMalloc(&d->sa, sab));
+        HIPCHK(hipMemcpy(d->sa, h.sa32.empty() ? (const void *)h.sa64.data() : (const void *)h.sa32.data(), sab,
+                         hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&d->pac, h.pac.size() + 16));
+        HIPCHK(hipMemcpy(d->pac, h.pac.data(), h.pac.size(), hipMemcpyHostToDevice));
+    }
+    DIndex &v = d->view;
+    v.occ = d->occ;
+    v.sa32 = h.sa32.empty() ? nullptr : (const uint32_t *)d->sa;
+    v.sa64 = h.sa32.empty() ? (const uint64_t *)d->sa : nullptr;
+    v.pac = d->pac;
+    v.ann_off = d->ann_off;
+    v.ann_len = d->ann_len;
+    v.n_anns = (int32_t)h.anns.size();
+    for (int c = 0; c < 5; ++c) v.L2[c] = h.L2[c];
+    v.primary = h.primary;
+    v.seq_len = h.seq_len;
+    v.l_pac = h.l_pac;
+    return BSQ_OK;
+}
+
+// ================================================================================================
+// lrand48 (Q10): X_{k+1} = (0x5DEECE66D X_k + 0xB) mod 2^48 from X_0 = 0, value X >> 17
+// ================================================================================================
+static uint64_t lrand48_state_at(uint64_t calls)
+{
+    const uint64_t M = (1ULL << 48) - 1;
+    uint64_t C = 0, a = 0x5DEECE66DULL, c = 0xB, e = calls;
+    while (e) {
+        if (e & 1) C = (a * C + c) & M;
+        c = (a * c + c) & M;
+        a = (a * a) & M;
+        e >>= 1;
+    }
+    return C;
+}
+extern "C" int64_t bsq_lrand48_at(uint64_t pos) { return (int64_t)(lrand48_state_at(pos + 1) >> 17); }
+
+// ================================================================================================
+// batch workspace
+// ================================================================================================
+namespace {
+
+struct Workspace {
+    Caps cp{};
+    int32_t max_reads = 0;
+    int grid = 0;
+    int64_t scratch_total = 0;
+    uint32_t *status = nullptr;
+    Intv *intv = nullptr;
+    int32_t *n_intv = nullptr, *n_chains = nullptr, *n_regs = nullptr, *n_cig = nullptr;
+    ChainDesc *chains = nullptr;
+    Seed *seeds = nullptr;
+    Reg *regs = nullptr;
+    Hit *hits = nullptr;
+    uint32_t *cigars = nullptr;
+    uint8_t *scratch = nullptr;
+    int32_t *sel = nullptr;   // local slot -> read (retry workspace only)
+
+    void release()
+    {
+        hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
+        hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
+        *this = Workspace{};
+    }
+};
+
+int64_t scratch_bytes(const Caps &c, int64_t z_cap)
+{
+    int64_t smem = 3LL * (c.max_len + 2) * (int64_t)sizeof(Intv);
+    int64_t chain = (int64_t)c.seeds * 24 + (int64_t)c.chains * 40 + (int64_t)(c.chains / 2 + 8) * 84 + 2LL * c.chains * 4;
+    int64_t ext = (int64_t)c.regs * (int64_t)sizeof(Reg) + ((c.regs * 4 + 15) & ~15) + (int64_t)c.seeds * 8 +
+                  (int64_t)(c.max_len + 2) * 8;
+    int64_t r2a = (((int64_t)(c.max_len + 2) * 8 + 63) & ~63LL) + z_cap;
+    int64_t m = std::max(std::max(smem, chain), std::max(ext, r2a));
+    return (m + 255) & ~255LL;
+}
+
+int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64_t z_cap, bool with_sel)
+{
+    w.cp = cp;
+    w.cp.scratch = scratch_bytes(cp, z_cap);
+    w.max_reads = max_reads;
+    int threads = std::min<int64_t>(std::max(max_reads, 1), workers);
+    w.grid = (threads + 255) / 256;
+    const size_t R = (size_t)std::max(max_reads, 1);
+    HIPCHK(hipMalloc(&w.status, R * 4));
+    HIPCHK(hipMalloc(&w.intv, R * cp.intv * sizeof(Intv)));
+    HIPCHK(hipMalloc(&w.n_intv, R * 4));
+    HIPCHK(hipMalloc(&w.n_chains, R * 4));
+    HIPCHK(hipMalloc(&w.n_regs, R * 4));
+    HIPCHK(hipMalloc(&w.n_cig, R * 4));
+    HIPCHK(hipMalloc(&w.chains, R * cp.chains * sizeof(ChainDesc)));
+    HIPCHK(hipMalloc(&w.seeds, R * cp.seeds * sizeof(Seed)));
+    HIPCHK(hipMalloc(&w.regs, R * cp.regs * sizeof(Reg)));
+    HIPCHK(hipMalloc(&w.hits, R * cp.regs * sizeof(Hit)));
+    HIPCHK(hipMalloc(&w.cigars, R * cp.regs * cp.cigar * 4));
+    w.scratch_total = (int64_t)w.grid * 256 * w.cp.scratch;
+    HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
+    if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
+    return BSQ_OK;
+}
+
+DOpts make_dopts(const bsq_opts &o)
+{
+    DOpts d{};
+    d.a = o.a; d.b = o.b; d.o_del = o.o_del; d.e_del = o.e_del; d.o_ins = o.o_ins; d.e_ins = o.e_ins;
+    d.pen_clip5 = o.pen_clip5; d.pen_clip3 = o.pen_clip3; d.w = o.w; d.zdrop = o.zdrop;
+    d.min_seed_len = o.min_seed_len; d.max_occ = o.max_occ;
+    d.split_width = 10; d.max_chain_gap = 10000; d.min_chain_weight = 0; d.max_chain_extend = 1 << 30;
+    d.max_mem_intv = 20; d.split_factor = 1.5f; d.mask_level = 0.50f; d.drop_ratio = 0.50f; d.mask_level_redun = 0.95f;
+    // mem_opt_init fills mat with a=1, b=4 and bioseqdb never refills it (Q2)
+    d.mat_match = 1; d.mat_mismatch = -4; d.mat_amb = -1; d.mat_max = 1;
+    return d;
+}
+
+}  // namespace
+
+struct bsq_batch {
+    bsq_index *idx = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int32_t max_reads = 0;
+    int64_t max_bases = 0;
+    int32_t n_reads = 0;
+    int32_t max_len = 0;
+    uint8_t *codes = nullptr;
+    int64_t *offs = nullptr;
+    int64_t *ids = nullptr;
+    std::vector<int64_t> h_offs;
+    std::vector<uint8_t> h_codes;   // kept for the retry pass
+    Workspace main, retry;
+    Counters *ctr = nullptr;
+    // packing
+    int64_t *cnt_hits = nullptr, *cnt_cig = nullptr, *off_hits = nullptr, *off_cig = nullptr;
+    unsigned long long *unresolved = nullptr;
+    int32_t *ovf_list = nullptr, *ovf_count = nullptr;
+    void *cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    bsq_hit *d_out = nullptr;
+    uint32_t *d_out_cig = nullptr;
+    int64_t out_cap = 0, out_cig_cap = 0;
+    bsq_hit *h_pinned = nullptr;
+    uint32_t *h_pinned_cig = nullptr;
+    int64_t h_cap = 0, h_cig_cap = 0;
+    // results
+    std::vector<bsq_hit> res_hits;
+    std::vector<uint32_t> res_cig;
+    std::vector<int64_t> res_off;
+    bsq_hits view{};
+    hipEvent_t ev[STG_N + 1]{};
+    float stage_ms[STG_N]{};
+    double stage_bytes[STG_N]{};
+    int64_t retried = 0;
+};
+
+static const char *kStageNames[STG_N] = {"smem", "chain", "extend", "reg2aln", "pack", "d2h"};
+extern "C" const char *bsq_stage_name(int s) { return (s >= 0 && s < STG_N) ? kStageNames[s] : ""; }
+
+static Caps main_caps(int max_len)
+{
+    Caps c{};
+    c.max_len = max_len;
+    c.intv = 64 + max_len / 4;
+    c.seeds = 256 + max_len;
+    c.chains = 64;
+    c.regs = 16;
+    c.cigar = 40;
+    return c;
+}
+
+static Caps retry_caps(int max_len)
+{
+    Caps c{};
+    c.max_len = max_len;
+    c.intv = 4 * max_len + 64;
+    c.seeds = 32768;
+    c.chains = 32768;
+    c.regs = 2048;
+    c.cigar = 2 * max_len + 8;
+    return c;
+}
+
+static int device_workers(int device)
+{
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return 65536;
+    return p.multiProcessorCount * 1024;
+}
+
+extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_bases, bsq_batch **out)
+{
+    if (!idx || !out || max_reads < 0 || max_bases < 0) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (!idx->h.dev) { set_err("index not uploaded to a device"); return BSQ_E_INVALID; }
+    bsq_batch *b = new (std::nothrow) bsq_batch();
+    if (!b) { set_err("out of memory"); return BSQ_E_NOMEM; }
+    b->idx = idx;
+    b->device = idx->h.dev->device;
+    b->max_reads = max_reads;
+    b->max_bases = max_bases;
+    *out = b;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    for (auto &e : b->ev) HIPCHK(hipEventCreate(&e));
+    const size_t R = (size_t)std::max(max_reads, 1);
+    HIPCHK(hipMalloc(&b->codes, (size_t)std::max<int64_t>(max_bases, 1)));
+    HIPCHK(hipMalloc(&b->offs, (R + 1) * 8));
+    HIPCHK(hipMalloc(&b->ids, R * 8));
+    HIPCHK(hipMalloc(&b->ctr, sizeof(Counters) * STG_N));
+    HIPCHK(hipMalloc(&b->cnt_hits, (R + 1) * 8));
+    HIPCHK(hipMalloc(&b->cnt_cig, (R + 1) * 8));
+    HIPCHK(hipMalloc(&b->off_hits, (R + 1) * 8));
+    HIPCHK(hipMalloc(&b->off_cig, (R + 1) * 8));
+    HIPCHK(hipMalloc(&b->unresolved, 8));
+    HIPCHK(hipMalloc(&b->ovf_list, R * 4));
+    HIPCHK(hipMalloc(&b->ovf_count, 4));
+    size_t t1 = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, b->cnt_hits, b->off_hits, (int)(R + 1), b->stream));
+    b->cub_bytes = t1;
+    HIPCHK(hipMalloc(&b->cub_tmp, b->cub_bytes));
+    return BSQ_OK;
+}
+
+extern "C" void bsq_batch_free(bsq_batch *b)
+{
+    if (!b) return;
+    hipSetDevice(b->device);
+    if (b->stream) hipStreamSynchronize(b->stream);
+    b->main.release();
+    b->retry.release();
+    hipFree(b->codes); hipFree(b->offs); hipFree(b->ids); hipFree(b->ctr);
+    hipFree(b->cnt_hits); hipFree(b->cnt_cig); hipFree(b->off_hits); hipFree(b->off_cig); hipFree(b->unresolved);
+    hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
+    hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig);
+    for (auto &e : b->ev) if (e) hipEventDestroy(e);
+    if (b->stream) hipStreamDestroy(b->stream);
+    delete b;
+}
+
+extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int64_t *offsets, int32_t n_reads)
+{
+    if (!b || (n_reads > 0 && (!codes || !offsets)) || n_reads < 0) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (n_reads > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
+    int64_t total = n_reads ? offsets[n_reads] - offsets[0] : 0;
+    if (total > b->max_bases) { set_err("batch holds at most %lld bases", (long long)b->max_bases); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    b->h_offs.assign(offsets, offsets + n_reads + 1);
+    int max_len = 0;
+    for (int i = 0; i < n_reads; ++i) {
+        int64_t l = offsets[i + 1] - offsets[i];
+        if (l < 0) { set_err("negative read length at %d", i); return BSQ_E_INVALID; }
+        max_len = std::max<int64_t>(max_len, l);
+    }
+    const int64_t base0 = n_reads ? offsets[0] : 0;
+    for (auto &o : b->h_offs) o -= base0;
+    b->h_codes.assign(codes + base0, codes + base0 + total);
+    b->n_reads = n_reads;
+    b->max_len = max_len;
+    if (n_reads) {
+        HIPCHK(hipMemcpyAsync(b->codes, b->h_codes.data(), (size_t)total, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (size_t)(n_reads + 1) * 8, hipMemcpyHostToDevice, b->stream));
+    }
+    // (re)allocate the main workspace for this read length
+    if (!b->main.status || b->main.cp.max_len < max_len) {
+        b->main.release();
+        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->max_reads, device_workers(b->device), 32 * 1024, false);
+        if (rc) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return BSQ_OK;
+}
+
+// Runs smem -> chain -> extend -> reg2aln on workspace w for n local reads.
+static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const int32_t *sel, bool timed)
+{
+    const DIndex &ix = b->idx->h.dev->view;
+    hipStream_t st = b->stream;
+    HIPCHK(hipMemsetAsync(w.status, 0, (size_t)std::max(n, 1) * 4, st));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
+    HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
+    HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, b->offs, sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
+                        w.scratch, b->ctr));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
+    HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, b->ids, n, w.chains, w.seeds, w.n_chains, w.regs,
+                         w.n_regs, w.status, w.scratch, b->ctr));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
+    HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
+                          w.status, w.scratch, b->ctr));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_PACK], st));
+    return BSQ_OK;
+}
+
+// Packs workspace w (n local reads) into host vectors hits/cig/off (hits with read_index = local).
+static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vector<bsq_hit> &hits,
+                        std::vector<uint32_t> &cig, std::vector<int64_t> &off, bool allow_unresolved)
+{
+    hipStream_t st = b->stream;
+    SlotView v{w.hits, w.cigars, w.n_regs, w.n_cig, w.cp};
+    HIPCHK(hipMemsetAsync(b->unresolved, 0, 8, st));
+    HIPCHK(hipMemsetAsync(b->cnt_hits + n, 0, 8, st));
+    HIPCHK(hipMemsetAsync(b->cnt_cig + n, 0, 8, st));
+    if (n) HIPCHK(launch_counts(st, n, v, v, nullptr, w.status, b->cnt_hits, b->cnt_cig, b->unresolved));
+    size_t tb = b->cub_bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->cub_tmp, tb, b->cnt_hits, b->off_hits, n + 1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->cub_tmp, tb, b->cnt_cig, b->off_cig, n + 1, st));
+    int64_t tot[2];
+    unsigned long long unres = 0;
+    HIPCHK(hipMemcpyAsync(&tot[0], b->off_hits + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&tot[1], b->off_cig + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&unres, b->unresolved, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (unres && !allow_unresolved) { set_err("%llu reads exceeded even the retry capacities", unres); return BSQ_E_UNSUPPORTED; }
+    if (tot[0] > b->out_cap) {
+        hipFree(b->d_out);
+        b->out_cap = std::max<int64_t>(tot[0], 2 * b->out_cap);
+        HIPCHK(hipMalloc(&b->d_out, (size_t)b->out_cap * sizeof(bsq_hit)));
+    }
+    if (tot[1] > b->out_cig_cap) {
+        hipFree(b->d_out_cig);
+        b->out_cig_cap = std::max<int64_t>(tot[1], 2 * b->out_cig_cap);
+        HIPCHK(hipMalloc(&b->d_out_cig, (size_t)b->out_cig_cap * 4));
+    }
+    if (tot[0] > b->h_cap) {
+        hipHostFree(b->h_pinned);
+        b->h_cap = std::max<int64_t>(tot[0], 2 * b->h_cap);
+        HIPCHK(hipHostMalloc((void **)&b->h_pinned, (size_t)b->h_cap * sizeof(bsq_hit)));
+    }
+    if (tot[1] > b->h_cig_cap) {
+        hipHostFree(b->h_pinned_cig);
+        b->h_cig_cap = std::max<int64_t>(tot[1], 2 * b->h_cig_cap);
+        HIPCHK(hipHostMalloc((void **)&b->h_pinned_cig, (size_t)b->h_cig_cap * 4));
+    }
+    const DeviceIndex *d = b->idx->h.dev;
+    if (n && tot[0]) HIPCHK(launch_pack(st, n, v, v, nullptr, b->off_hits, b->off_cig, d->ann_off, d->ann_id, b->d_out, b->d_out_cig));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_D2H], st));
+    off.resize((size_t)n + 1);
+    HIPCHK(hipMemcpyAsync(off.data(), b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
+    if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_N], st));
+    HIPCHK(hipStreamSynchronize(st));
+    hits.assign(b->h_pinned, b->h_pinned + tot[0]);
+    cig.assign(b->h_pinned_cig, b->h_pinned_cig + tot[1]);
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq)
+{
+    if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len <= 0) {
+        set_err("gap extension penalties, max_occ and min_seed_len must be positive");
+        return BSQ_E_INVALID;
+    }
+    if (b->max_len >= 700) {   // mem_flt_chained_seeds becomes active: not implemented on this path yet
+        double l = b->max_len;
+        if (!(5.5 * std::log(l) > 0.05 * l)) { set_err("reads of %d bp need mem_flt_chained_seeds (unsupported)", b->max_len); return BSQ_E_UNSUPPORTED; }
+    }
+    HIPCHK(hipSetDevice(b->device));
+    const int n = b->n_reads;
+    const DOpts o = make_dopts(*opts);
+    hipStream_t st = b->stream;
+    // lrand48 ids: read i consumes call first_call_seq + i
+    {
+        std::vector<int64_t> ids((size_t)std::max(n, 1));
+        const uint64_t M = (1ULL << 48) - 1;
+        uint64_t X = lrand48_state_at(first_call_seq);
+        for (int i = 0; i < n; ++i) { X = (0x5DEECE66DULL * X + 0xB) & M; ids[i] = (int64_t)(X >> 17); }
+        if (n) HIPCHK(hipMemcpyAsync(b->ids, ids.data(), (size_t)n * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    b->retried = 0;
+    b->res_hits.clear(); b->res_cig.clear(); b->res_off.assign((size_t)n + 1, 0);
+    int rc = BSQ_OK;
+    if (n > 0 && b->idx->h.seq_len > 0) {
+        rc = run_stages(b, b->main, o, n, nullptr, true);
+        if (rc) return rc;
+        // overflowing reads -> retry workspace with large capacities
+        HIPCHK(hipMemsetAsync(b->ovf_count, 0, 4, st));
+        HIPCHK(launch_collect_overflow(st, n, b->main.status, b->ovf_list, b->ovf_count));
+        int32_t novf = 0;
+        HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true);
+        if (rc) return rc;
+        if (novf > 0) {
+            b->retried = novf;
+            std::vector<int32_t> list((size_t)novf);
+            HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
+            std::sort(list.begin(), list.end());
+            const int CH = 256;
+            if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
+                b->retry.release();
+                rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
+                if (rc) return rc;
+            }
+            // per-read replacement results
+            std::vector<std::vector<bsq_hit>> rh((size_t)novf);
+            std::vector<std::vector<uint32_t>> rcg((size_t)novf);
+            for (int s = 0; s < novf; s += CH) {
+                int m = std::min(CH, novf - s);
+                HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
+                rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
+                if (rc) return rc;
+                std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
+                rc = pack_to_host(b, b->retry, m, false, hh, cc, oo, false);
+                if (rc) return rc;
+                for (int j = 0; j < m; ++j) {
+                    auto &dst = rh[(size_t)(s + j)];
+                    auto &dc = rcg[(size_t)(s + j)];
+                    for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
+                        bsq_hit x = hh[(size_t)k];
+                        uint32_t base = (uint32_t)dc.size();
+                        dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
+                        x.cigar_off = base;
+                        dst.push_back(x);
+                    }
+                }
+            }
+            // merge into read order
+            std::vector<bsq_hit> mh; std::vector<uint32_t> mc; std::vector<int64_t> mo((size_t)n + 1, 0);
+            size_t li = 0;
+            for (int r = 0; r < n; ++r) {
+                mo[r] = (int64_t)mh.size();
+                if (li < list.size() && list[li] == r) {
+                    for (auto x : rh[li]) {
+                        uint32_t base = (uint32_t)mc.size();
+                        mc.insert(mc.end(), rcg[li].begin() + x.cigar_off, rcg[li].begin() + x.cigar_off + x.n_cigar);
+                        x.cigar_off = base; x.read_index = r;
+                        mh.push_back(x);
+                    }
+                    ++li;
+                } else {
+                    for (int64_t k = b->res_off[r]; k < b->res_off[r + 1]; ++k) {
+                        bsq_hit x = b->res_hits[(size_t)k];
+                        uint32_t base = (uint32_t)mc.size();
+                        mc.insert(mc.end(), b->res_cig.begin() + x.cigar_off, b->res_cig.begin() + x.cigar_off + x.n_cigar);
+                        x.cigar_off = base;
+                        mh.push_back(x);
+                    }
+                }
+            }
+            mo[n] = (int64_t)mh.size();
+            b->res_hits.swap(mh); b->res_cig.swap(mc); b->res_off.swap(mo);
+        }
+        // stage timings + algorithmic bytes
+        for (int s = 0; s < STG_N; ++s) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, b->ev[s], b->ev[s + 1]);
+            b->stage_ms[s] = ms;
+        }
+        Counters c[STG_N];
+        HIPCHK(hipMemcpy(c, b->ctr, sizeof c, hipMemcpyDeviceToHost));
+        b->stage_bytes[STG_SMEM] = 64.0 * c[STG_SMEM].occ_blocks + (double)b->h_offs[n] / 4.0 * 1.0;
+        b->stage_bytes[STG_CHAIN] = 8.0 * c[STG_CHAIN].sa_values;
+        b->stage_bytes[STG_EXTEND] = (double)c[STG_EXTEND].ref_bases;
+        b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;
+        b->stage_bytes[STG_PACK] = (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
+        b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
+    } else {
+        for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; }
+    }
+    b->view.n_reads = n;
+    b->view.n_hits = (int64_t)b->res_hits.size();
+    b->view.hits = b->res_hits.data();
+    b->view.read_off = b->res_off.data();
+    b->view.n_cigar = (int64_t)b->res_cig.size();
+    b->view.cigar = b->res_cig.data();
+    return BSQ_OK;
+}
+
+extern "C" const bsq_hits *bsq_batch_hits(const bsq_batch *b) { return b ? &b->view : nullptr; }
+
+extern "C" int bsq_batch_stage_ms(const bsq_batch *b, float *ms, int max)
+{
+    if (!b) return 0;
+    for (int s = 0; s < STG_N && s < max; ++s) ms[s] = b->stage_ms[s];
+    return STG_N;
+}
+
+extern "C" int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max)
+{
+    if (!b) return 0;
+    for (int s = 0; s < STG_N && s < max; ++s) bytes[s] = b->stage_bytes[s];
+    return STG_N;
+}
+
+extern "C" int64_t bsq_batch_retried(const bsq_batch *b) { return b ? b->retried : -1; }
+
+// ================================================================================================
+// one-shot API
+// ================================================================================================
+extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                               uint64_t first_call_seq, bsq_hits **out)
+{
+    if (!idx || !opts || !out || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *out = nullptr;
+    std::vector<uint8_t> codes;
+    std::vector<int64_t> offs((size_t)n_reads + 1, 0);
+    for (int i = 0; i < n_reads; ++i) {
+        ns_to_nt4(static_cast<const uint8_t *>(reads[i]), codes);
+        offs[i + 1] = (int64_t)codes.size();
+    }
+    bsq_hits *h = (bsq_hits *)calloc(1, sizeof(bsq_hits));
+    if (!h) { set_err("out of memory"); return BSQ_E_NOMEM; }
+    h->n_reads = n_reads;
+    if (!idx->h.built) { free(h); set_err("index not built"); return BSQ_E_INVALID; }
+    if (idx->h.seq_len == 0 || n_reads == 0) {   // empty reference: align_sequence returns {} (bwa.cpp:191)
+        h->read_off = (int64_t *)calloc((size_t)n_reads + 1, 8);
+        *out = h;
+        return BSQ_OK;
+    }
+    if (!idx->h.dev) { free(h); set_err("index not uploaded to a device (call bsq_index_upload)"); return BSQ_E_NODEV; }
+    bsq_batch *b = nullptr;
+    int rc = bsq_batch_create(idx, n_reads, (int64_t)codes.size(), &b);
+    if (rc == BSQ_OK) rc = bsq_batch_set_reads(b, codes.data(), offs.data(), n_reads);
+    if (rc == BSQ_OK) rc = bsq_batch_run(b, opts, first_call_seq);
+    if (rc != BSQ_OK) { bsq_batch_free(b); free(h); return rc; }
+    h->n_hits = b->view.n_hits;
+    h->n_cigar = b->view.n_cigar;
+    h->hits = (bsq_hit *)malloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
+    h->cigar = (uint32_t *)malloc(4 * (size_t)std::max<int64_t>(h->n_cigar, 1));
+    h->read_off = (int64_t *)malloc(8 * ((size_t)n_reads + 1));
+    memcpy(h->hits, b->view.hits, sizeof(bsq_hit) * (size_t)h->n_hits);
+    memcpy(h->cigar, b->view.cigar, 4 * (size_t)h->n_cigar);
+    memcpy(h->read_off, b->view.read_off, 8 * ((size_t)n_reads + 1));
+    bsq_batch_free(b);
+    *out = h;
+    return BSQ_OK;
+}
+
+extern "C" void bsq_hits_free(bsq_hits *h)
+{
+    if (!h) return;
+    free(h->hits); free(h->cigar); free(h->read_off); free(h);
+}

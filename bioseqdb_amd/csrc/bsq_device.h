@@ -1,0 +1,82 @@
+// bsq_device.h -- data layouts shared by the host driver (bsq_api.cpp) and the HIP kernels
+// (align_kernels.hip).  Everything here is plain-old-data so the same bytes are valid on both sides.
+#pragma once
+#include <stdint.h>
+
+namespace bsq {
+
+// One occurrence block of the $-removed BWT: 128 rows, 64 bytes.  cnt[c] = number of base c in
+// rows before the block; the 128 bases are stored as two bit-planes (hi, lo) so a rank query is
+// three 128-bit popcounts.  Same rank function as libbwa's bwt_occ4 (bwt.c), different bits.
+struct alignas(64) OccBlock {
+    uint64_t cnt[4];
+    uint64_t hi[2];
+    uint64_t lo[2];
+};
+static_assert(sizeof(OccBlock) == 64, "occ block must be one 64-byte sector");
+
+// Device view of the index (passed by value as a kernel argument).
+struct DIndex {
+    const OccBlock *occ;
+    const uint32_t *sa32;     // full suffix array of T$ (rows 0..seq_len) when seq_len < 2^32
+    const uint64_t *sa64;     // otherwise
+    const uint8_t *pac;       // forward pac, 4 bases per byte, MSB first (sequence.h:55)
+    const int64_t *ann_off;   // bntann1_t.offset per reference row
+    const int32_t *ann_len;   // bntann1_t.len
+    int32_t n_anns;
+    int32_t pad;
+    uint64_t L2[5];
+    uint64_t primary, seq_len;
+    int64_t l_pac;
+};
+
+// mem_opt_t fields the path reads (mem_opt_init defaults + bioseqdb overrides).
+struct DOpts {
+    int32_t a, b, o_del, e_del, o_ins, e_ins, pen_clip5, pen_clip3, w, zdrop;
+    int32_t min_seed_len, max_occ, split_width, max_chain_gap, min_chain_weight, max_chain_extend, max_mem_intv;
+    float split_factor, mask_level, drop_ratio, mask_level_redun;
+    int32_t mat_match, mat_mismatch, mat_amb, mat_max;   // the 5x5 matrix from bwa_fill_scmat (Q2)
+};
+
+// Per-batch capacities (the main pass uses small ones; overflowing reads are re-run with large ones).
+struct Caps {
+    int32_t max_len;     // longest read in the batch
+    int32_t intv;        // SMEM intervals per read
+    int32_t seeds;       // seeds per read after SA expansion
+    int32_t chains;      // chains per read
+    int32_t regs;        // alignment regions per read
+    int32_t cigar;       // CIGAR ops per region
+    int64_t scratch;     // bytes of private scratch per worker thread
+};
+
+struct Intv { uint64_t x[3]; uint64_t info; };
+struct Seed { int64_t rbeg; int32_t qbeg, len; };
+struct ChainDesc { int32_t seed_off, n, rid, w; };
+
+struct Reg {
+    int64_t rb, re;
+    int32_t qb, qe, rid, score, truesc, sub, csub, sub_n, w, seedcov, secondary, seedlen0, n_comp, pad;
+    uint64_t hash;
+};
+
+struct Hit {            // one region after mem_reg2aln
+    int64_t rb, re;
+    int32_t qb, qe, rid, score, flag, is_rev, n_cigar, pad;
+};
+
+// status bits per read
+enum : uint32_t { ST_OVERFLOW = 1u, ST_UNSUPPORTED = 2u };
+
+enum Stage { STG_SMEM = 0, STG_CHAIN, STG_EXTEND, STG_REG2ALN, STG_PACK, STG_D2H, STG_N };
+
+// device-side algorithmic byte counters, one slot per stage
+struct Counters {
+    unsigned long long occ_blocks;   // 64-B occ block fetches in bwt_extend
+    unsigned long long sa_values;    // SA values produced
+    unsigned long long ref_bases;    // reference bases fetched for extension / CIGAR
+    unsigned long long dp_cells;     // DP cells evaluated (secondary figure)
+    unsigned long long overflow;     // reads flagged for the retry pass
+    unsigned long long pad[3];
+};
+
+}  // namespace bsq

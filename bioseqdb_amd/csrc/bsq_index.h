@@ -1,0 +1,66 @@
+// bsq_index.h -- host-side index object behind the C-ABI (replaces bioseqdb's BwaIndex storage,
+// bioseqdb/bwa.h:32-48, and libbwa's bwt_t/bntseq_t built in BwaIndex::build, bwa.cpp:156-177).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "bsq_device.h"
+
+namespace bsq {
+
+struct Hole { int64_t offset; int32_t len; char amb; };           // bntamb1_t
+struct Ann { int64_t offset; int32_t len, n_ambs; int64_t id; };    // bntann1_t subset (name = id)
+
+// nuclseq varlena accessors (sequence.h:18-38, 55-61)
+inline uint32_t ns_holes_num(const uint8_t *ns) { uint32_t v; __builtin_memcpy(&v, ns + 4, 4); return v; }
+inline uint32_t ns_len(const uint8_t *ns) { uint32_t v; __builtin_memcpy(&v, ns + 8, 4); return v; }
+inline const uint8_t *ns_pac(const uint8_t *ns) { return ns + 12 + 16 * (size_t)ns_holes_num(ns); }
+inline Hole ns_hole(const uint8_t *ns, uint32_t i)
+{
+    Hole h; const uint8_t *p = ns + 12 + 16 * (size_t)i;
+    __builtin_memcpy(&h.offset, p, 8); __builtin_memcpy(&h.len, p + 8, 4); h.amb = (char)p[12];
+    return h;
+}
+inline size_t pac_byte_size(size_t x) { return x / 4 + (x % 4 != 0 ? 1 : 0); }
+inline int pac_get(const uint8_t *pac, uint64_t i) { return pac[i >> 2] >> ((~i & 3) << 1) & 3; }
+inline int nt4(unsigned char c)
+{
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    case '-': return 5;
+    default: return 4;
+    }
+}
+// to_text rendering (sequence.cpp:71-81) and nt4 coding of a read (bwa.cpp:195 + mem_align1_core)
+std::string ns_to_text(const uint8_t *ns);
+void ns_to_nt4(const uint8_t *ns, std::vector<uint8_t> &out);
+
+struct DeviceIndex;   // bsq_api.cpp
+
+struct HostIndex {
+    std::vector<uint8_t> pac;    // pac_forward
+    std::vector<Hole> holes;     // unshifted offsets (Q3)
+    std::vector<Ann> anns;
+    bool built = false;
+    int64_t l_pac = 0;
+    uint64_t seq_len = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
+    std::vector<OccBlock> occ;
+    std::vector<uint32_t> sa32;  // full SA of T$ when seq_len < 2^32
+    std::vector<uint64_t> sa64;
+    DeviceIndex *dev = nullptr;
+
+    void add_ref(int64_t id, const uint8_t *ns);
+    int build(int threads, std::string &err);
+    uint64_t sa(uint64_t row) const { return sa32.empty() ? sa64[row] : sa32[row]; }
+    void occ4(uint64_t k, uint64_t c[4]) const;
+};
+
+}  // namespace bsq
+
+// opaque C-ABI handle (include/bsq.h)
+struct bsq_index { bsq::HostIndex h; };

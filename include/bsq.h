@@ -1,0 +1,155 @@
+/*
+ * bsq.h -- C-ABI of libbsq, the MI355X-native BWA-MEM alignment path behind bioseqdb's
+ * nuclseq_search_bwa / nuclseq_multi_search_bwa.
+ *
+ * Every entry point is plain C (pointers, sizes, status codes; no C++ types, exceptions or
+ * longjmp cross it).  Each one replaces a piece of the reference's in-process seam
+ * (bioseqdb/bwa.h:32-48 `class BwaIndex` over libbwa):
+ *
+ *   bsq_index_create / bsq_index_free  <- BwaIndex::BwaIndex / ~BwaIndex        (bwa.cpp:129, 180-188)
+ *   bsq_index_add_ref                  <- BwaIndex::add_ref_sequence            (bwa.cpp:131-154)
+ *   bsq_index_build                    <- BwaIndex::build                       (bwa.cpp:156-177)
+ *                                         = pac2bwt + is_bwt + bwt_bwtupdate_core + bwt_cal_sa
+ *   bsq_index_upload                   <- (new) copies BWT/occ, SA and pac into HBM once
+ *   bsq_align_batch                    <- BwaIndex::align_sequence per read     (bwa.cpp:190-230)
+ *                                         = mem_align1 + mem_reg2aln for a whole cursor batch
+ *   bsq_render_tsv                     <- the BwaMatch rendering of align_sequence
+ *                                         (extract_reference_subseq, cigar_compressed_to_string)
+ *   bsq_opts                           <- the mem_opt_t fields set by bwa_index_from_query
+ *                                         (extension.cpp:211-236; effective values incl. Q1)
+ *
+ * Status codes: BSQ_OK (0) or a negative BSQ_E_*; bsq_last_error() gives a thread-local message.
+ * Ownership: inputs are borrowed for the duration of the call; outputs are allocated by libbsq and
+ * released with the matching *_free.  An index is immutable after bsq_index_upload; concurrent
+ * bsq_align_* calls on one index from different host threads are safe (each batch has its own
+ * stream and workspace).
+ */
+#ifndef BSQ_H
+#define BSQ_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSQ_OK 0
+#define BSQ_E_INVALID (-1)   /* bad argument / state */
+#define BSQ_E_NOMEM (-2)     /* host or device allocation failed */
+#define BSQ_E_HIP (-3)       /* HIP runtime error */
+#define BSQ_E_NODEV (-4)     /* no usable gfx950 device */
+#define BSQ_E_UNSUPPORTED (-5) /* input outside what the path implements (e.g. reads >= 700 bp) */
+
+/* Effective BWA-MEM options (mem_opt_t fields bioseqdb writes, extension.cpp:220-231).  The SQL
+ * bwa_opts() field-order quirk (Q1) is applied by the caller: defaults are
+ * {19, max(500, 2*n_refs), 1, 4, 5, 5, 100, 100, o_del=6, e_del=6, o_ins=1, e_ins=1}. */
+typedef struct {
+    int32_t min_seed_len, max_occ, a, b, pen_clip3, pen_clip5, zdrop, w, o_del, e_del, o_ins, e_ins;
+} bsq_opts;
+
+typedef struct bsq_index bsq_index;
+typedef struct bsq_batch bsq_batch;
+
+/* One alignment region = one bwa_result row (bioseqdb--0.0.0.sql:196-212).  Coordinates are the
+ * reference's: rb/re in the forward+reverse space [0, 2*l_pac) (Q6). */
+typedef struct {
+    int64_t ref_id;            /* anns[rid].name reinterpreted as int64 (bwa.cpp:209) */
+    int64_t rb, re;            /* mem_alnreg_t rb/re */
+    int32_t ref_match_start;   /* (int32)(rb - anns[rid].offset)  */
+    int32_t ref_match_end;     /* (int32)(re - anns[rid].offset)  */
+    int32_t ref_match_len;     /* (int32)(re - rb)                */
+    int32_t qb, qe;            /* query_match_start / _end        */
+    int32_t score;             /* mem_aln_t.score = mem_alnreg_t.score (Q9) */
+    int32_t rid;
+    uint8_t is_primary, is_secondary, is_reverse, pad0;
+    int32_t read_index;        /* index of the read within the batch */
+    uint32_t cigar_off, n_cigar; /* into bsq_hits.cigar: u32 len<<4 | op, ops 0..4 = M,I,D,S(clip=3),H */
+} bsq_hit;
+
+typedef struct {
+    int32_t n_reads;
+    int64_t n_hits;
+    bsq_hit *hits;             /* read order, then libbwa's final region order (Q16) */
+    int64_t *read_off;         /* n_reads+1: hits of read i are [read_off[i], read_off[i+1]) */
+    int64_t n_cigar;
+    uint32_t *cigar;
+} bsq_hits;
+
+const char *bsq_last_error(void);
+const char *bsq_version(void);
+/* Number of HIP devices visible (0 without a GPU; never initialises a device context). */
+int bsq_device_count(void);
+
+/* ---- nuclseq codec (the type's text I/O; reference: nuclseq_from_text sequence.cpp:209-245 with
+ * std::minstd_rand(holes_num ^ len) fill of hole and padding bases, and to_text_palloc :71-81) ---- */
+/* Encodes len characters (nst_nt4 ACGT -> 2-bit, anything else -> run-length hole) into a malloc'd
+ * NucleotideSequence varlena; size in *out_size.  No validation of the alphabet (nuclseq_in does it). */
+void *bsq_nuclseq_from_text(const char *text, size_t len, size_t *out_size);
+/* Renders a NucleotideSequence varlena as text (malloc'd, NUL-terminated). */
+char *bsq_nuclseq_to_text(const void *nuclseq);
+
+/* ---- index ----------------------------------------------------------------------------------- */
+int bsq_index_create(bsq_index **out);
+void bsq_index_free(bsq_index *idx);
+/* `nuclseq` points at a detoasted NucleotideSequence varlena (sequence.h:18-38):
+ * {vl_len[4], holes_num u32, len u32, holes_num x bntamb1_t(16 B), ceil(len/4) pac bytes}. */
+int bsq_index_add_ref(bsq_index *idx, int64_t id, const void *nuclseq);
+/* Host build of T = pac || revcomp(pac), its suffix array, BWT, occ blocks.  `threads` <= 0: all cores. */
+int bsq_index_build(bsq_index *idx, int threads);
+/* Copies the built index into HBM of `device`. */
+int bsq_index_upload(bsq_index *idx, int device);
+int64_t bsq_index_l_pac(const bsq_index *idx);
+int64_t bsq_index_seq_len(const bsq_index *idx);
+int64_t bsq_index_primary(const bsq_index *idx);
+int32_t bsq_index_n_refs(const bsq_index *idx);
+/* Host copies of the logical FM quantities for tests (valid after build, no GPU needed):
+ * sa[row] for row in [0, seq_len] and occ4 per row. */
+int64_t bsq_index_sa(const bsq_index *idx, int64_t row);
+int bsq_index_occ4(const bsq_index *idx, int64_t k, uint64_t cnt[4]);
+/* Export the full suffix array (seq_len+1 entries of `*elem_bytes` = 4 or 8 bytes); borrowed. */
+const void *bsq_index_sa_data(const bsq_index *idx, int *elem_bytes);
+
+/* ---- alignment --------------------------------------------------------------------------------- */
+/* Value of the (pos+1)-th lrand48() call of an unseeded glibc/musl process (Q10). */
+int64_t bsq_lrand48_at(uint64_t pos);
+
+/* Align n_reads nuclseq reads (each a NucleotideSequence varlena pointer).  Read i uses the
+ * lrand48 value of call number first_call_seq + i (mem_align1's mem_mark_primary_se id).
+ * On success *out holds every region of every read. */
+int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                    uint64_t first_call_seq, bsq_hits **out);
+void bsq_hits_free(bsq_hits *hits);
+
+/* Renders hits as bwa_result rows (TSV, one line per hit, columns as bioseqdb--0.0.0.sql:196-212
+ * without query_id): ref_id ref_subseq ref_match_start ref_match_end ref_match_len query_subseq
+ * query_match_start query_match_end query_match_len is_primary is_secondary is_reverse cigar score.
+ * ref_subseq on reverse-strand rows, where the reference reads out of bounds (Q7), is rendered
+ * as the reverse-strand reference text.  Returns a malloc'd string (free with bsq_free). */
+char *bsq_render_tsv(const bsq_index *idx, const bsq_hits *hits, const void *const *reads);
+void bsq_free(void *p);
+
+/* ---- device-resident batches (bench / multi-GPU drivers) --------------------------------------- */
+/* A batch owns a HIP stream and a device workspace for up to max_reads reads / max_bases bases. */
+int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_bases, bsq_batch **out);
+void bsq_batch_free(bsq_batch *b);
+/* Stage reads given as nt4 codes (0..3 = ACGT, 4 = other), offsets[n+1] (host arrays) into HBM. */
+int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int64_t *offsets, int32_t n_reads);
+/* Run the whole alignment pipeline on the staged reads and copy the packed hits to the host. */
+int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq);
+/* Borrowed view of the last run's hits (valid until the next run or free). */
+const bsq_hits *bsq_batch_hits(const bsq_batch *b);
+/* Per-stage device time of the last run in ms, measured with HIP events on the batch stream.
+ * Writes up to `max` values; returns the number of stages; names via bsq_stage_name(). */
+int bsq_batch_stage_ms(const bsq_batch *b, float *ms, int max);
+const char *bsq_stage_name(int stage);
+/* Algorithmic bytes of the last run (SURVEY.md §8(d) counting), per stage: occ-block fetches x64,
+ * SA values x8, reference windows ceil(bases/4), reads and hit records.  Returns stages written. */
+int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max);
+/* Number of reads of the last run that needed the large-capacity retry pass. */
+int64_t bsq_batch_retried(const bsq_batch *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
