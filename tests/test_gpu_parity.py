@@ -1,0 +1,97 @@
+"""GPU (HIP) path vs the CPU oracle on seeded synthetic inputs: every bwa_result column must match
+bit for bit (ref_subseq excluded on reverse rows, Q7)."""
+import random
+
+import numpy as np
+import pytest
+
+from bioseqdb_amd import synth
+from parity_util import build_pair, compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _texts(reads):
+    return [reads.text(i) for i in range(reads.n)]
+
+
+def test_parity_small_synthetic():
+    ref = synth.make_reference(200_000, n_rows=1, n_run_every=100_000, n_run_len=300)
+    reads = synth.make_reads(ref, 3000, seed=11)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=0)
+    assert rows > 2500
+    assert not bad, bad[:20]
+
+
+def test_parity_c1_config():
+    """BASELINE.json configs[0] shape: 10k x 150 bp reads vs a 1 Mbp reference."""
+    ref = synth.make_reference(1_000_000)
+    reads = synth.make_reads(ref, 10_000)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=123)
+    assert rows > 9000
+    assert not bad, bad[:20]
+
+
+def test_parity_multi_row_padding_holes():
+    """Several rows with lengths not multiple of 4 (Q4 padding), IUPAC holes (Q3/Q5), tiny rows."""
+    rng = random.Random(5)
+    rows = []
+    for L in (50_001, 7, 30_002, 0, 41_003, 120):
+        s = [rng.choice("ACGT") for _ in range(L)]
+        for _ in range(L // 5000):
+            p = rng.randrange(max(L - 40, 1))
+            ch = rng.choice("NRYKMSWBDHV")
+            for j in range(p, min(p + rng.randint(1, 30), L)):
+                s[j] = ch
+        rows.append("".join(s))
+    # reads sampled across rows, some spanning row boundaries, some with IUPAC symbols
+    cat = "".join(rows)
+    reads = []
+    comp = str.maketrans("ACGTNRYKMSWBDHV", "TGCANYRMKSWVHDB")
+    for i in range(1500):
+        L = rng.choice([150, 150, 100, 60, 33, 19, 18, 250])
+        p = rng.randrange(max(len(cat) - L, 1))
+        r = list(cat[p:p + L])
+        for j in range(len(r)):
+            if rng.random() < 0.02:
+                r[j] = rng.choice("ACGT")
+        r = "".join(r)
+        if rng.random() < 0.5:
+            r = r.translate(comp)[::-1]
+        reads.append(r)
+    pi, oi = build_pair(rows, ids=[11, -3, 2 ** 40, 7, 99, 5])
+    nrows, bad = compare(pi, oi, reads, first_call=7)
+    assert nrows > 1000
+    assert not bad, bad[:20]
+
+
+def test_parity_repeats_secondaries():
+    """Tandem and interspersed repeats: many chains, secondaries, hash tie-breaks (Q10)."""
+    rng = random.Random(9)
+    unit = "".join(rng.choice("ACGT") for _ in range(300))
+    parts = []
+    for k in range(40):
+        parts.append("".join(rng.choice("ACGT") for _ in range(rng.randint(200, 3000))))
+        u = list(unit)
+        for j in range(len(u)):
+            if rng.random() < 0.01:
+                u[j] = rng.choice("ACGT")
+        parts.append("".join(u))
+    ref = "".join(parts)
+    reads = []
+    for i in range(1500):
+        p = rng.randrange(len(ref) - 150)
+        r = list(ref[p:p + 150])
+        for j in range(150):
+            if rng.random() < 0.01:
+                r[j] = rng.choice("ACGT")
+        if rng.random() < 0.1:
+            q = rng.randrange(20, 130)
+            del r[q:q + rng.randint(1, 3)]
+        reads.append("".join(r))
+    pi, oi = build_pair([ref])
+    nrows, bad = compare(pi, oi, reads, first_call=1000)
+    assert nrows > 1500
+    assert not bad, bad[:20]
