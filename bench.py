@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: aligned reads/s, 150 bp synthetic reads vs a 100 Mbp synthetic
+reference, full BWA-MEM seed + extend + CIGAR (configs[2], "C3"), on N MI355X GPUs.
+
+One step = one pass of the whole alignment path (libbsq: smem -> chain -> extend -> reg2aln -> pack ->
+D2H of the hit records) over one batch of reads already resident in HBM; with N > 1 each rank aligns
+its own batch (weak scaling, read-sharded) and the hit records are gathered to rank 0 over RCCL
+(the exchange step of the SQL path: all rows return to the calling backend).
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, algorithmic bytes / HIP-event time on
+the batch stream) and `cpu_baseline` (the CPU oracle on this host's cores, bounded sample, rank 0 at
+N = 1 only; its outputs are also checksummed against the GPU's for the same reads).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from bioseqdb_amd import synth  # noqa: E402
+from bioseqdb_amd import _native as N  # noqa: E402
+
+METRIC = "aligned reads/sec (150 bp vs 100 Mbp ref) at 1/2/4/8 MI355X; bit-exact vs libbwa"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def default_opts(n_refs: int) -> N.Opts:
+    # effective SQL defaults incl. the bwa_opts() field-order quirk (Q1): e_del=6, o_ins=1
+    return N.Opts(19, max(500, 2 * n_refs), 1, 4, 5, 5, 100, 100, 6, 6, 1, 1)
+
+
+def fnv(h: int, v: int) -> int:
+    for i in range(8):
+        h ^= (v >> (8 * i)) & 0xFF
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def gpu_checksum(hits: "N.Hits", n_reads: int) -> int:
+    """Same per-read FNV hash the oracle's orc_align_batch computes (order-independent sum)."""
+    H = hits
+    ck = 0
+    for r in range(n_reads):
+        h = fnv(0xCBF29CE484222325, r)
+        for k in range(H.read_off[r], H.read_off[r + 1]):
+            x = H.hits[k]
+            for v in (x.rb, x.re, x.qb & 0xFFFFFFFF, x.qe & 0xFFFFFFFF, x.score & 0xFFFFFFFF,
+                      0x100 if x.is_secondary else 0):
+                h = fnv(h, v & 0xFFFFFFFFFFFFFFFF)
+            for c in range(x.n_cigar):
+                h = fnv(h, H.cigar[x.cigar_off + c])
+        ck = (ck + h) & 0xFFFFFFFFFFFFFFFF
+    return ck
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU per step")
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--ref-bp", type=int, default=100_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    L = N.lib()
+    t0 = time.time()
+    ref = synth.make_reference(args.ref_bp)
+    reads = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + rank)
+    t_gen = time.time() - t0
+
+    # ---- index (host build, the step before the hot path) + HBM upload ----
+    idx = ctypes.c_void_p()
+    N.check(L.bsq_index_create(ctypes.byref(idx)))
+    ref_ns = []
+    for i, t in enumerate(ref.texts()):
+        size = ctypes.c_size_t()
+        p = L.bsq_nuclseq_from_text(t, len(t), ctypes.byref(size))
+        buf = ctypes.create_string_buffer(ctypes.string_at(p, size.value), size.value)
+        L.bsq_free(p)
+        ref_ns.append(buf)
+        N.check(L.bsq_index_add_ref(idx, i + 1, ctypes.addressof(buf)))
+    t0 = time.time()
+    N.check(L.bsq_index_build(idx, 0))
+    t_build = time.time() - t0
+    t0 = time.time()
+    N.check(L.bsq_index_upload(idx, local))
+    t_upload = time.time() - t0
+    opts = default_opts(len(ref.rows))
+
+    # ---- batch: reads resident in HBM before timing ----
+    batch = ctypes.c_void_p()
+    N.check(L.bsq_batch_create(idx, reads.n, int(reads.offsets[-1]), ctypes.byref(batch)))
+    codes = np.ascontiguousarray(reads.codes)
+    offs = np.ascontiguousarray(reads.offsets)
+    N.check(L.bsq_batch_set_reads(batch, codes.ctypes.data, offs.ctypes.data, reads.n))
+    first_call = rank * reads.n    # lrand48 stream position as one backend aligning all ranks' reads in order
+    log(f"[bench r{rank}] gen {t_gen:.1f}s index build {t_build:.1f}s upload {t_upload:.2f}s "
+        f"seq_len {L.bsq_index_seq_len(idx)}")
+
+    def step():
+        N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
+        if dist is not None:
+            import torch
+            H = L.bsq_batch_hits(batch).contents
+            nbytes = H.n_hits * ctypes.sizeof(N.Hit)
+            host = np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)),
+                                         shape=(max(nbytes, 1),))
+            cnt = torch.tensor([nbytes], device="cuda", dtype=torch.int64)
+            cnts = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(cnts, cnt)
+            mx = int(max(int(c.item()) for c in cnts))
+            send = torch.zeros(max(mx, 1), dtype=torch.uint8, device="cuda")
+            if nbytes:
+                send[:nbytes].copy_(torch.from_numpy(host[:nbytes].copy()), non_blocking=False)
+            recv = torch.empty(world * max(mx, 1), dtype=torch.uint8, device="cuda")
+            dist.all_gather_into_tensor(recv, send)
+            if rank == 0:
+                recv.cpu()
+
+    for _ in range(args.warmup):
+        step()
+    stage_ms = np.zeros(6)
+    stage_bytes = np.zeros(6)
+    if dist is not None:
+        import torch
+        dist.barrier()
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        ms = (ctypes.c_float * 6)()
+        L.bsq_batch_stage_ms(batch, ms, 6)
+        by = (ctypes.c_double * 6)()
+        L.bsq_batch_stage_bytes(batch, by, 6)
+        stage_ms += np.array(list(ms))
+        stage_bytes += np.array(list(by))
+    if dist is not None:
+        import torch
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stage_ms /= max(args.steps, 1)
+    stage_bytes /= max(args.steps, 1)
+    H = L.bsq_batch_hits(batch).contents
+    n_hits = int(H.n_hits)
+    retried = int(L.bsq_batch_retried(batch))
+    names = [L.bsq_stage_name(i).decode() for i in range(6)]
+    kern = {names[i]: float(stage_ms[i]) for i in range(4)}
+    dom = max(kern, key=kern.get)
+    di = names.index(dom)
+    achieved = stage_bytes[di] / (stage_ms[di] * 1e-3) / 1e9 if stage_ms[di] > 0 else 0.0
+
+    total_reads = args.reads * world
+    value = total_reads * args.steps / elapsed
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "reads/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C3: 150 bp reads vs 100 Mbp synthetic reference, full seed + banded SW extension + CIGAR "
+                        "(BASELINE.json configs[2]); bwa_opts() SQL defaults",
+            "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
+            "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "algorithmic_bytes_per_launch": float(stage_bytes[di]), "launch_ms": round(float(stage_ms[di]), 3),
+        },
+        "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
+        "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
+        "index_build_s": round(t_build, 2),
+        "retried_reads": retried,
+    }
+
+    # ---- CPU baseline: the oracle on this host, bounded sample, rank 0 at N = 1 only ----
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py as O
+        oi = O.OracleIndex()
+        for buf in ref_ns:
+            oi.add_ref(len(oi._keep) + 1, bytes(buf.raw))
+        eb = ctypes.c_int()
+        sa = L.bsq_index_sa_data(idx, ctypes.byref(eb))
+        oi.build_from_sa(sa, eb.value)
+        oo = O.opts_from(opts)
+        ncpu = os.cpu_count() or 1
+        threads = args.cpu_threads or min(16, ncpu)
+
+        def run_cpu(n, th):
+            ck = ctypes.c_uint64()
+            t = time.perf_counter()
+            nreg = O.lib().orc_align_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, 0, th,
+                                           ctypes.byref(ck))
+            return time.perf_counter() - t, nreg, ck.value
+
+        dt, _, _ = run_cpu(min(2000, reads.n), threads)            # calibration / warm-up
+        rate = min(2000, reads.n) / max(dt, 1e-6)
+        sample = int(min(reads.n, max(2000, rate * args.cpu_seconds)))
+        dt, nreg, ck = run_cpu(sample, threads)
+        dt1, _, _ = run_cpu(min(500, reads.n), 1)
+        gck = gpu_checksum(H, sample)
+        result["cpu_baseline"] = {
+            "value": round(sample / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} reads of the same batch, CPU oracle (oracle/bwa_oracle.c, -O2), "
+                      f"{threads} threads; 1-thread rate {round(min(500, reads.n) / dt1, 1)} reads/s on 500 reads",
+            "value_1thread": round(min(500, reads.n) / dt1, 1),
+        }
+        result["parity_sample"] = {"reads": sample, "regions": int(nreg), "checksum_match": bool(gck == ck)}
+        result["gpu_vs_cpu"] = round(value / (sample / dt), 1)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    L.bsq_batch_free(batch)
+    L.bsq_index_free(idx)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
