@@ -124,23 +124,15 @@ def main() -> int:
 
     def step():
         N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
-        if dist is not None:
+        if dist is not None:   # exchange step: hit records + CIGARs of every rank to the caller
             import torch
+            from bioseqdb_amd import dist as D
             H = L.bsq_batch_hits(batch).contents
-            nbytes = H.n_hits * ctypes.sizeof(N.Hit)
-            host = np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)),
-                                         shape=(max(nbytes, 1),))
-            cnt = torch.tensor([nbytes], device="cuda", dtype=torch.int64)
-            cnts = [torch.zeros_like(cnt) for _ in range(world)]
-            dist.all_gather(cnts, cnt)
-            mx = int(max(int(c.item()) for c in cnts))
-            send = torch.zeros(max(mx, 1), dtype=torch.uint8, device="cuda")
-            if nbytes:
-                send[:nbytes].copy_(torch.from_numpy(host[:nbytes].copy()), non_blocking=False)
-            recv = torch.empty(world * max(mx, 1), dtype=torch.uint8, device="cuda")
-            dist.all_gather_into_tensor(recv, send)
-            if rank == 0:
-                recv.cpu()
+            nb = H.n_hits * ctypes.sizeof(N.Hit)
+            nc = H.n_cigar * 4
+            hb = np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb]
+            cb = np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc]
+            D.gather_records(np.concatenate([hb, cb]), device=torch.device("cuda", local))
 
     for _ in range(args.warmup):
         step()

@@ -161,7 +161,7 @@ extern "C" int64_t bsq_index_sa(const bsq_index *idx, int64_t row)
 extern "C" int bsq_index_occ4(const bsq_index *idx, int64_t k, uint64_t cnt[4])
 {
     if (!idx || !idx->h.built || idx->h.seq_len == 0) { set_err("index not built"); return BSQ_E_INVALID; }
-    if (k < -1 || (uint64_t)k > idx->h.seq_len) { set_err("row out of range"); return BSQ_E_INVALID; }
+    if (k < -1 || (k >= 0 && (uint64_t)k > idx->h.seq_len)) { set_err("row out of range"); return BSQ_E_INVALID; }
     idx->h.occ4((uint64_t)k, cnt);
     return BSQ_OK;
 }

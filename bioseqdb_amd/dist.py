@@ -1,0 +1,54 @@
+"""Read-sharded multi-GPU driver (one process per GPU, torch.distributed over RCCL or gloo).
+
+The SQL path is embarrassingly parallel over query rows (extension.cpp:362-370 aligns one cursor row
+at a time and libbwa keeps no cross-read state except the lrand48 position, Q10).  Each rank takes a
+contiguous slice of the reads, aligns it on its own GPU against its own replica of the index, and the
+hit records travel to rank 0 (the calling backend) in one all-gather, which preserves read order
+(rank order == read order, Q16).  No other collective sits on the data path.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+def shard(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous read range [lo, hi) of `rank` among `world` ranks."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def first_call_of(rank: int, world: int, n_total: int, base: int = 0) -> int:
+    """lrand48 stream position of the shard's first read: as if one backend aligned all reads in order."""
+    return base + shard(n_total, rank, world)[0]
+
+
+def gather_records(local: np.ndarray, group=None, device=None) -> List[np.ndarray]:
+    """All-gather variable-length uint8 record buffers; returns them in rank order (valid on every rank).
+
+    Works with the "nccl" (RCCL, tensors on `device`) and "gloo" (CPU tensors) backends: one
+    all-gather of the byte counts, one all-gather of the buffers padded to the largest."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = device if device is not None else torch.device("cpu")
+    n = torch.tensor([local.nbytes], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes_i = [int(s.item()) for s in sizes]
+    mx = max(max(sizes_i), 1)
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    if local.nbytes:
+        buf[:local.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(local).view(np.uint8).reshape(-1)))
+    out = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    return [o[:s].cpu().numpy() for o, s in zip(out, sizes_i)]
+
+
+def merge_rows(per_rank: Sequence[Sequence[tuple]]) -> List[tuple]:
+    """Concatenate per-rank result rows in rank (= read) order."""
+    out: List[tuple] = []
+    for rows in per_rank:
+        out.extend(rows)
+    return out

@@ -1,0 +1,52 @@
+"""Host-side mirror of the reference interface (no GPU): options, cursor semantics, errors."""
+import pytest
+
+from bioseqdb_amd import bwa as B
+from bioseqdb_amd import (BwaOptions, NucleotideSequence, bwa_opts, effective_opts, lrand48_calls,
+                          nuclseq_multi_search_bwa, nuclseq_search_bwa, reset_lrand48)
+
+
+def test_bwa_opts_field_order_quirk_q1():
+    o = bwa_opts()
+    # ROW(..., o_del, o_ins, e_del, e_ins) cast positionally onto (..., o_del, e_del, o_ins, e_ins)
+    assert (o.o_del, o.e_del, o.o_ins, o.e_ins) == (6, 6, 1, 1)
+    e = effective_opts(o, n_refs=3)
+    assert (e.min_seed_len, e.max_occ, e.a, e.b, e.pen_clip3, e.pen_clip5, e.zdrop, e.w) == (19, 500, 1, 4, 5, 5, 100, 100)
+    assert (e.o_del, e.e_del, e.o_ins, e.e_ins) == (6, 6, 1, 1)
+    o2 = bwa_opts(o_del=7, o_ins=8, e_del=2, e_ins=3)
+    assert (o2.o_del, o2.e_del, o2.o_ins, o2.e_ins) == (7, 8, 2, 3)
+
+
+def test_max_occ_default_q11():
+    assert effective_opts(bwa_opts(), n_refs=10).max_occ == 500
+    assert effective_opts(bwa_opts(), n_refs=400).max_occ == 800
+    assert effective_opts(bwa_opts(max_occ=7), n_refs=400).max_occ == 7
+
+
+def test_null_fields_take_defaults_negative_rejected():
+    e = effective_opts(BwaOptions(*([None] * 12)), n_refs=1)
+    assert (e.min_seed_len, e.o_del, e.e_del, e.o_ins, e.e_ins) == (19, 6, 1, 6, 1)   # get_opt_or defaults
+    with pytest.raises(B.InvalidParameterValue, match="bwa_opt zdrop must be nonnegative"):
+        effective_opts(bwa_opts(zdrop=-1), n_refs=1)
+
+
+def test_cursor_rows_nulls_and_types_q14():
+    s = NucleotideSequence.from_text("ACGT")
+    rows = list(B._iterate_nuclseq_table([(1, s), (None, s), (2, None), (3, s)]))
+    assert [r for r, _ in rows] == [1, 3]
+    with pytest.raises(B.DatatypeMismatch, match="expected column of integers"):
+        list(B._iterate_nuclseq_table([("x", s)]))
+    with pytest.raises(B.DatatypeMismatch, match="expected column of nuclseqs"):
+        list(B._iterate_nuclseq_table([(1, "ACGT")]))
+
+
+def test_empty_reference_returns_no_rows_and_no_lrand48_call():
+    reset_lrand48(5)
+    q = NucleotideSequence.from_text("ACGT" * 40)
+    assert nuclseq_search_bwa(q, []) == []
+    assert nuclseq_multi_search_bwa([(1, q), (2, q)], [(1, NucleotideSequence.from_text(""))]) == []
+    assert lrand48_calls() == 5   # align_sequence returns before mem_align1 (bwa.cpp:191)
+
+
+def test_result_columns():
+    assert B.BWA_RESULT_COLUMNS[5] == "query_id" and len(B.BWA_RESULT_COLUMNS) == 15

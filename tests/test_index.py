@@ -1,0 +1,72 @@
+"""Product index builder (libbsq host code) vs the oracle's independent suffix sort (no GPU)."""
+import ctypes
+import random
+
+import pytest
+
+import oracle_py as O
+from bioseqdb_amd import BwaIndex, NucleotideSequence
+from bioseqdb_amd._native import lib
+
+
+def both(rows):
+    pi, oi = BwaIndex(), O.OracleIndex()
+    for k, t in enumerate(rows):
+        ns = NucleotideSequence.from_text(t)
+        pi.add_ref_sequence(k + 1, ns)
+        oi.add_ref(k + 1, ns.raw)
+    pi.build(threads=3)
+    oi.build()
+    return pi, oi
+
+
+def rand_rows(rng, n_rows, max_len, holes=True):
+    rows = []
+    for _ in range(n_rows):
+        L = rng.randint(0, max_len)
+        s = [rng.choice("ACGT") for _ in range(L)]
+        if holes:
+            for _ in range(rng.randint(0, 3)):
+                if L > 10:
+                    p = rng.randrange(L - 6)
+                    ch = rng.choice("NRYKMSWBDHV")
+                    for j in range(p, p + rng.randint(1, 6)):
+                        s[j] = ch
+        rows.append("".join(s))
+    return rows
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_sa_occ_l2_equal_oracle(seed):
+    rng = random.Random(seed)
+    rows = rand_rows(rng, rng.randint(1, 5), 2500)
+    if seed == 5:
+        rows = ["A" * 700, "ACGT" * 300, "GATTACA" * 50]   # low-complexity: long tie groups in the suffix sort
+    pi, oi = both(rows)
+    h = pi.handle
+    n = lib().bsq_index_seq_len(h)
+    assert n == oi.seq_len
+    if n == 0:
+        return
+    assert lib().bsq_index_primary(h) == oi.primary
+    for r in range(1, n + 1):                   # row 0 is the $ row; libbwa stores sa[0] = -1 there
+        assert lib().bsq_index_sa(h, r) == oi.sa(r)
+    c = (ctypes.c_uint64 * 4)()
+    for k in range(-1, n + 1):
+        assert lib().bsq_index_occ4(h, k, c) == 0
+        assert list(c) == oi.occ4(k), k
+
+
+def test_concatenation_quirks_q3_q4():
+    """Rows are appended byte-aligned (Q4): l_pac = 4 * sum(ceil(len/4)); offsets = 4 * bytes so far."""
+    rows = ["ACGTA", "", "CC", "ACGTACGT"]
+    pi, oi = both(rows)
+    assert pi.l_pac == 4 * (2 + 0 + 1 + 2) == oi.l_pac
+    assert lib().bsq_index_n_refs(pi.handle) == 4
+
+
+def test_empty_reference_builds_nothing():
+    pi, _ = both(["", ""])
+    assert pi.l_pac == 0 and lib().bsq_index_seq_len(pi.handle) == 0
+    assert pi.align_sequences([NucleotideSequence.from_text("ACGT" * 10)], pi.options or
+                              __import__("bioseqdb_amd").effective_opts(None, 2)) == [[]]
