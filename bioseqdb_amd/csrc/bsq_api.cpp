@@ -40,6 +40,8 @@ hipError_t launch_counts(hipStream_t, int, const SlotView &, const SlotView &, c
 hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const int64_t *,
                        const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *);
 hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
+hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
+                           Intv *, int32_t *, uint32_t *, Counters *, int);
 }  // namespace bsq
 
 using namespace bsq;
@@ -361,9 +363,15 @@ struct bsq_batch {
 static const char *kStageNames[STG_N] = {"smem", "chain", "extend", "reg2aln", "pack", "d2h"};
 extern "C" const char *bsq_stage_name(int s) { return (s >= 0 && s < STG_N) ? kStageNames[s] : ""; }
 
+static bool tiny_caps() { const char *e = getenv("BSQ_TEST_TINY_CAPS"); return e && *e && *e != '0'; }
+
 static Caps main_caps(int max_len)
 {
     Caps c{};
+    if (tiny_caps()) {   // test knob: force most reads through the overflow -> retry path
+        c.max_len = max_len; c.intv = 6; c.seeds = 8; c.chains = 2; c.regs = 1; c.cigar = 6;
+        return c;
+    }
     c.max_len = max_len;
     c.intv = 64 + max_len / 4;
     c.seeds = 256 + max_len;
@@ -465,7 +473,7 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
         HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (size_t)(n_reads + 1) * 8, hipMemcpyHostToDevice, b->stream));
     }
     // (re)allocate the main workspace for this read length
-    if (!b->main.status || b->main.cp.max_len < max_len) {
+    if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1)) {
         b->main.release();
         int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->max_reads, device_workers(b->device), 32 * 1024, false);
         if (rc) return rc;
@@ -481,7 +489,13 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     hipStream_t st = b->stream;
     HIPCHK(hipMemsetAsync(w.status, 0, (size_t)std::max(n, 1) * 4, st));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
-    HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
+    if (!sel && w.cp.max_len < 65536) {
+        // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
+        const int lcap = tiny_caps() ? 3 : ix.seq_len < 0xFFFFFFFFull ? 28 : 16;
+        HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap));
+    } else {
+        HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
+    }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
     HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, b->offs, sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
                         w.scratch, b->ctr));

@@ -95,3 +95,15 @@ def test_parity_repeats_secondaries():
     nrows, bad = compare(pi, oi, reads, first_call=1000)
     assert nrows > 1500
     assert not bad, bad[:20]
+
+
+def test_parity_retry_path_tiny_caps(monkeypatch):
+    """Shrink every main-pass slot so nearly all reads overflow and go through the large-capacity
+    retry kernels; results must be unchanged."""
+    monkeypatch.setenv("BSQ_TEST_TINY_CAPS", "1")
+    ref = synth.make_reference(150_000, n_run_every=60_000, n_run_len=200)
+    reads = synth.make_reads(ref, 700, seed=23)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=55)
+    assert rows > 600
+    assert not bad, bad[:20]
