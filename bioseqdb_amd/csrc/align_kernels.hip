@@ -15,22 +15,13 @@
 #include <stdint.h>
 
 #include "bsq_device.h"
+#include "dev_common.h"
 #include "../../include/bsq.h"
 
 namespace bsq {
 
 #define DEV __device__ __forceinline__
 #define DEVN __device__ __noinline__
-
-// ------------------------------------------------------------------------------------------------
-// reference text access (bntseq.c _get_pac / bns_get_seq semantics)
-// ------------------------------------------------------------------------------------------------
-DEV int pac_get(const uint8_t *pac, int64_t i) { return (pac[i >> 2] >> ((~i & 3) << 1)) & 3; }
-// base of the forward+reverse text at coordinate p in [0, 2*l_pac)
-DEV int ref_at(const DIndex &ix, int64_t p)
-{
-    return p < ix.l_pac ? pac_get(ix.pac, p) : 3 - pac_get(ix.pac, (ix.l_pac << 1) - 1 - p);
-}
 
 // ------------------------------------------------------------------------------------------------
 // FM index: rank over the $-removed BWT (same function as libbwa bwt_occ4)
@@ -201,17 +192,6 @@ DEV int seed_strategy1(const DIndex &ix, int len, const uint8_t *q, int x, int m
 }
 
 // ------------------------------------------------------------------------------------------------
-// wave-aggregated counter add (one atomic per wave and counter)
-// ------------------------------------------------------------------------------------------------
-DEV void wave_add(unsigned long long *dst, unsigned long long v)
-{
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
-}
-
-DEV int read_of(const int32_t *sel, int i) { return sel ? sel[i] : i; }
-
-// ------------------------------------------------------------------------------------------------
 // k_smem: mem_collect_intv per read
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_smem(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
@@ -358,38 +338,6 @@ DEV void ks_introsort(int *a, int n, LT lt)
             --top; s = stk_l[top]; t = stk_r[top]; d = stk_d[top];
         }
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// bntseq helpers
-// ------------------------------------------------------------------------------------------------
-DEV int64_t depos(const DIndex &ix, int64_t pos, int &is_rev)
-{
-    return (is_rev = (pos >= ix.l_pac)) ? (ix.l_pac << 1) - 1 - pos : pos;
-}
-
-DEV int pos2rid(const DIndex &ix, int64_t pos_f)
-{
-    if (pos_f >= ix.l_pac) return -1;
-    int left = 0, mid = 0, right = ix.n_anns;
-    while (left < right) {
-        mid = (left + right) >> 1;
-        if (pos_f >= ix.ann_off[mid]) {
-            if (mid == ix.n_anns - 1) break;
-            if (pos_f < ix.ann_off[mid + 1]) break;
-            left = mid + 1;
-        } else right = mid;
-    }
-    return mid;
-}
-
-DEV int intv2rid(const DIndex &ix, int64_t rb, int64_t re)
-{
-    int is_rev;
-    if (rb < ix.l_pac && re > ix.l_pac) return -2;
-    int rid_b = pos2rid(ix, depos(ix, rb, is_rev));
-    int rid_e = rb < re ? pos2rid(ix, depos(ix, re - 1, is_rev)) : rid_b;
-    return rid_b == rid_e ? rid_b : -1;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -689,31 +637,68 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
 // ------------------------------------------------------------------------------------------------
 // ksw_extend2 / ksw_global2 (ksw.c) over accessor-defined query and target
 // ------------------------------------------------------------------------------------------------
-struct QAcc {   // query[j] = base[start + dir*j]
-    const uint8_t *base; int start, dir;
-    DEV int operator()(int j) const { return base[start + dir * j]; }
+// eh row storage for ksw_extend2: global int2, or LDS packed u16 pairs interleaved by lane
+// (lane l's column j at lds[j * 64 + l]: every lane hits its own bank, so accesses never conflict).
+// ksw_extend2 keeps h and e in [0, h0 + qlen*max] (every candidate is clamped at 0), so u16 is exact
+// whenever the host-side bound check passes.
+struct EhG {
+    int2 *p;
+    DEV int2 get(int j) const { return p[j]; }
+    DEV void set(int j, int2 v) const { p[j] = v; }
 };
-struct TAcc {   // target[i] = ref_at(start + dir*i)
-    const DIndex *ix; int64_t start; int dir;
-    DEV int operator()(int i) const { return ref_at(*ix, start + (int64_t)dir * i); }
+extern __shared__ uint32_t g_lds_eh[];   // dynamic LDS of k_extend<true>
+struct EhL {   // offset-based so the accesses stay in the LDS address space (ds_read/ds_write, not flat)
+    int base;
+    DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + j * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
+    DEV void set(int j, int2 v) const { g_lds_eh[base + j * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
-DEV int mat_sc(const DOpts &o, int t, int q)
-{
-    return (t == 4 || q == 4) ? o.mat_amb : (t == q ? o.mat_match : o.mat_mismatch);
-}
+// Sequential reader of the target bases target(i) = ref_at(start + dir*i), i = 0, 1, 2, ...: keeps the
+// current and the next 16-base pac word in registers so the per-row base never waits on memory.
+struct TStream {
+    const uint8_t *pac;
+    int64_t fp;         // forward-strand pac position of the next base
+    int fstep;          // +1 / -1 along the forward pac
+    int comp;           // 3 on the reverse strand (base = 3 - pac)
+    int64_t cur_w, max_w;
+    uint32_t cur, nxt;
+    DEV uint32_t load(int64_t w) const { return (w >= 0 && w <= max_w) ? *reinterpret_cast<const uint32_t *>(pac + 4 * w) : 0u; }
+    DEV void init(const DIndex &ix, int64_t start, int dir)
+    {
+        pac = ix.pac;
+        max_w = (ix.l_pac >> 4);
+        if (start < ix.l_pac) { fp = start; fstep = dir; comp = 0; }
+        else { fp = (ix.l_pac << 1) - 1 - start; fstep = -dir; comp = 3; }
+        cur_w = fp >> 4;
+        cur = load(cur_w);
+        nxt = load(cur_w + fstep);
+    }
+    DEV int next()
+    {
+        const int64_t w = fp >> 4;
+        if (w != cur_w) { cur = w == cur_w + fstep ? nxt : load(w); cur_w = w; nxt = load(w + fstep); }
+        const int byte = (int)((fp >> 2) & 3), sh = (int)((~fp & 3) << 1);
+        const int b = (int)((cur >> (8 * byte + sh)) & 3u);
+        fp += fstep;
+        return b ^ comp;
+    }
+};
 
+template <class EH>
 DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
                      int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
-                     int *_gscore, int *_max_off, int2 *eh, uint64_t &cells)
+                     int *_gscore, int *_max_off, EH eh, uint64_t &cells)
 {
     int i, j, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, beg, end, max, max_i, max_j, max_ins, max_del, max_ie,
         gscore, max_off;
     if (qlen < 0) qlen = 0;
-    for (j = 0; j <= qlen; ++j) eh[j] = make_int2(0, 0);
-    eh[0].x = h0;
-    if (qlen >= 1) eh[1].x = h0 > oe_ins ? h0 - oe_ins : 0;
-    for (j = 2; j <= qlen && eh[j - 1].x > e_ins; ++j) eh[j].x = eh[j - 1].x - e_ins;
+    {   // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
+        const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+        for (j = 0; j <= qlen; ++j) {
+            int h = j == 0 ? h0 : (j == 1 ? v1 : (v1 - (j - 1) * e_ins > 0 ? v1 - (j - 1) * e_ins : 0));
+            eh.set(j, make_int2(h, 0));
+        }
+    }
     max = o.mat_max > 0 ? o.mat_max : 0;
     max_ins = (int)((double)(qlen * max + end_bonus - o_ins) / e_ins + 1.);
     max_ins = max_ins > 1 ? max_ins : 1;
@@ -724,9 +709,11 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
     max = h0, max_i = max_j = -1; max_ie = -1, gscore = -1;
     max_off = 0;
     beg = 0, end = qlen;
+    TStream ts;
+    if (tlen > 0) ts.init(*target.ix, target.start, target.dir);
     for (i = 0; i < tlen; ++i) {
         int t, f = 0, h1, m = 0, mj = -1;
-        const int tb = target(i);
+        const int tb = ts.next();
         if (beg < i - w) beg = i - w;
         if (end > i + w + 1) end = i + w + 1;
         if (end > qlen) end = qlen;
@@ -736,7 +723,7 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
         } else h1 = 0;
         cells += (uint64_t)(end > beg ? end - beg : 0);
         for (j = beg; j < end; ++j) {
-            int2 p = eh[j];
+            int2 p = eh.get(j);
             int h, M = p.x, e = p.y;
             p.x = h1;
             M = M ? M + mat_sc(o, tb, query(j)) : 0;
@@ -748,11 +735,11 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
             t = M - oe_del; t = t > 0 ? t : 0;
             e -= e_del; e = e > t ? e : t;
             p.y = e;
-            eh[j] = p;
+            eh.set(j, p);
             t = M - oe_ins; t = t > 0 ? t : 0;
             f -= e_ins; f = f > t ? f : t;
         }
-        eh[end] = make_int2(h1, 0);
+        eh.set(end, make_int2(h1, 0));
         if (j == qlen) {
             max_ie = gscore > h1 ? max_ie : i;
             gscore = gscore > h1 ? gscore : h1;
@@ -769,9 +756,9 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
                 if (max - m - ((mj - max_j) - (i - max_i)) * e_ins > zdrop) break;
             }
         }
-        for (j = beg; j < end && eh[j].x == 0 && eh[j].y == 0; ++j);
+        for (j = beg; j < end; ++j) { int2 v = eh.get(j); if (v.x != 0 || v.y != 0) break; }
         beg = j;
-        for (j = end; j >= beg && eh[j].x == 0 && eh[j].y == 0; --j);
+        for (j = end; j >= beg; --j) { int2 v = eh.get(j); if (v.x != 0 || v.y != 0) break; }
         end = j + 2 < qlen ? j + 2 : qlen;
     }
     *_qle = max_j + 1;
@@ -927,8 +914,9 @@ struct ExtCtx {
     bool ovf;
 };
 
+template <class EH>
 DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
-                   ExtCtx &X, uint64_t &cells, uint64_t &bases)
+                   ExtCtx &X, EH ehx, uint64_t &cells, uint64_t &bases)
 {
     int64_t l_pac = ix.l_pac, rmax0, rmax1;
     if (c.n == 0) return;
@@ -1007,7 +995,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
                 int prev = a.score;
                 aw0 = o.w << t;
                 a.score = ksw_extend2(o, s.qbeg, qa, (int)tmp, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, aw0, o.pen_clip5,
-                                      o.zdrop, s.len * o.a, &qle, &tle, &gtle, &gscore, &max_off0, X.eh, cells);
+                                      o.zdrop, s.len * o.a, &qle, &tle, &gtle, &gscore, &max_off0, ehx, cells);
                 if (a.score == prev || max_off0 < (aw0 >> 1) + (aw0 >> 2)) break;
             }
             if (gscore <= 0 || gscore <= a.score - o.pen_clip5) {
@@ -1029,7 +1017,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
                 aw1 = o.w << t;
                 a.score = ksw_extend2(o, l_query - qe, qa, (int)(rmax1 - rmax0 - re), ta, o.o_del, o.e_del, o.o_ins,
                                       o.e_ins, aw1, o.pen_clip3, o.zdrop, sc0, &qle, &tle, &gtle, &gscore, &max_off1,
-                                      X.eh, cells);
+                                      ehx, cells);
                 if (a.score == prev || max_off1 < (aw1 >> 1) + (aw1 >> 2)) break;
             }
             if (gscore <= 0 || gscore <= a.score - o.pen_clip3) {
@@ -1171,10 +1159,12 @@ DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
     }
 }
 
-__global__ void __launch_bounds__(256) k_extend(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
-                                                const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
-                                                const Seed *seeds, const int32_t *n_chains, Reg *regs_out,
-                                                int32_t *n_regs, uint32_t *status, uint8_t *scratch, Counters *ctr)
+template <bool LDS>
+__global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
+                                                           const int64_t *offs, const int32_t *sel, const int64_t *ids,
+                                                           int n, const ChainDesc *chains, const Seed *seeds,
+                                                           const int32_t *n_chains, Reg *regs_out, int32_t *n_regs,
+                                                           uint32_t *status, uint8_t *scratch, Counters *ctr)
 {
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1196,7 +1186,13 @@ __global__ void __launch_bounds__(256) k_extend(DIndex ix, DOpts o, Caps cp, con
         const ChainDesc *cd = chains + (size_t)li * cp.chains;
         const Seed *sd = seeds + (size_t)li * cp.seeds;
         const int nc = n_chains[li];
-        for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, cells, bases);
+        if (LDS) {
+            EhL ehx{(int)threadIdx.x};   // blockDim == 64: lane-interleaved u16 pairs
+            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, cells, bases);
+        } else {
+            EhG ehx{X.eh};
+            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, cells, bases);
+        }
         if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
         X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
         mark_primary_se(o, X, ids[r]);
@@ -1209,16 +1205,6 @@ __global__ void __launch_bounds__(256) k_extend(DIndex ix, DOpts o, Caps cp, con
 // ------------------------------------------------------------------------------------------------
 // k_reg2aln: mem_reg2aln per region
 // ------------------------------------------------------------------------------------------------
-DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
-{
-    int w;
-    if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
-    w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
-    int d = l1 - l2; d = d < 0 ? -d : d;
-    if (w < d) w = d;
-    return w;
-}
-
 __global__ void __launch_bounds__(256) k_reg2aln(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                  const int32_t *sel, int n, const Reg *regs, const int32_t *n_regs,
                                                  Hit *hits, uint32_t *cigars, int32_t *n_cig_read, uint32_t *status,
@@ -1384,8 +1370,16 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
                          const Seed *seeds, const int32_t *n_chains, Reg *regs, int32_t *n_regs, uint32_t *status,
                          uint8_t *scratch, Counters *ctr)
 {
-    hipLaunchKernelGGL(k_extend, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds, n_chains,
-                       regs, n_regs, status, scratch, ctr);
+    // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
+    const bool lds = cp.max_len <= 200 && (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
+    if (lds) {
+        const size_t sh = (size_t)64 * (cp.max_len + 2) * 4;
+        hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
+                           seeds, n_chains, regs, n_regs, status, scratch, ctr);
+    } else {
+        hipLaunchKernelGGL(k_extend<false>, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds,
+                           n_chains, regs, n_regs, status, scratch, ctr);
+    }
     return hipGetLastError();
 }
 

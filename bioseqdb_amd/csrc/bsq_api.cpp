@@ -40,6 +40,9 @@ hipError_t launch_counts(hipStream_t, int, const SlotView &, const SlotView &, c
 hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const int64_t *,
                        const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *);
 hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
+hipError_t launch_reg2aln_w(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                            int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *, uint32_t *, Counters *, int,
+                            uint8_t *, int64_t, int);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int);
 }  // namespace bsq
@@ -76,6 +79,8 @@ extern "C" int bsq_device_count(void)
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
+
+static bool tiny_caps() { const char *e = getenv("BSQ_TEST_TINY_CAPS"); return e && *e && *e != '0'; }
 
 static int default_threads()
 {
@@ -262,11 +267,15 @@ struct Workspace {
     uint32_t *cigars = nullptr;
     uint8_t *scratch = nullptr;
     int32_t *sel = nullptr;   // local slot -> read (retry workspace only)
+    uint8_t *zslab = nullptr; // per-wave traceback spill slabs of the wave reg2aln kernel
+    int64_t zslab_bytes = 0;
+    int zslab_blocks = 0;
 
     void release()
     {
         hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
+        hipFree(zslab);
         *this = Workspace{};
     }
 };
@@ -304,6 +313,11 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     w.scratch_total = (int64_t)w.grid * 256 * w.cp.scratch;
     HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
     if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
+    if (!with_sel) {
+        w.zslab_bytes = (int64_t)(2 * cp.max_len + 8) * (int64_t)(2 * cp.max_len + 64);
+        w.zslab_blocks = (int)std::min<int64_t>(((int64_t)R + 3) / 4, 3 * 256);
+        HIPCHK(hipMalloc(&w.zslab, (size_t)w.zslab_blocks * 4 * (size_t)w.zslab_bytes));
+    }
     return BSQ_OK;
 }
 
@@ -362,8 +376,6 @@ struct bsq_batch {
 
 static const char *kStageNames[STG_N] = {"smem", "chain", "extend", "reg2aln", "pack", "d2h"};
 extern "C" const char *bsq_stage_name(int s) { return (s >= 0 && s < STG_N) ? kStageNames[s] : ""; }
-
-static bool tiny_caps() { const char *e = getenv("BSQ_TEST_TINY_CAPS"); return e && *e && *e != '0'; }
 
 static Caps main_caps(int max_len)
 {
@@ -503,8 +515,17 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, b->ids, n, w.chains, w.seeds, w.n_chains, w.regs,
                          w.n_regs, w.status, w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
-    HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
-                          w.status, w.scratch, b->ctr));
+    if (!sel && w.cp.max_len <= 1024) {
+        // main pass: one wave per read, DP rows across lanes, eh + traceback in LDS (dp_wave.hip)
+        const size_t eh_bytes = ((size_t)(w.cp.max_len + 2) * 8 + 15) & ~(size_t)15;
+        const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes) & ~15;
+        // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
+        HIPCHK(launch_reg2aln_w(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
+                                w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks));
+    } else {
+        HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars,
+                              w.n_cig, w.status, w.scratch, b->ctr));
+    }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_PACK], st));
     return BSQ_OK;
 }

@@ -1,0 +1,283 @@
+// dp_wave.hip -- wave-cooperative banded DP for mem_reg2aln (libbwa bwa_gen_cigar2 / ksw_global2).
+//
+// One 64-lane wave per read; the read's regions are processed in order with wave-uniform control
+// (every lane computes the same scalars) and lane-parallel DP rows:
+//   * lane l owns query column beg + 64*chunk + l of the current target row;
+//   * the ksw_global2 row state eh[0..qlen] (H(i-1,j-1), E(i,j)) lives in LDS, so cells outside the
+//     band keep exactly the values the serial kernel would leave there;
+//   * the F (insertion) recurrence F(j+1) = max(F(j) - e_ins, M(j) - oe_ins) is evaluated as an
+//     exclusive max-plus prefix scan across lanes, F(j) = max(F0 - (j-c0)e, max_{k<j}(t_k - (j-1-k)e));
+//   * the traceback matrix z (one byte per cell, same bits as ksw) is written row by row into LDS,
+//     coalesced, and walked back uniformly.
+// Integer arithmetic only; results equal the serial ksw_global2 cell for cell.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bsq_device.h"
+#include "dev_common.h"
+#include "../../include/bsq.h"
+
+namespace bsq {
+
+#define NEG_SCAN (-0x3fffffff - 0x3fffffff)   // scan identity far below any reachable value
+#define MINUS_INF_W (-0x40000000)
+
+DEV void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+DEV int lane_id() { return threadIdx.x & 63; }
+
+// wave64 exclusive max-scan with DPP (row_shr 1/2/4/8, row_bcast 15/31, wave_shr 1): gfx9-family
+#define DPP_STEP(v, ctrl, rmask) { int u_ = __builtin_amdgcn_update_dpp(NEG_SCAN, v, ctrl, rmask, 0xf, false); v = v > u_ ? v : u_; }
+DEV int wave_excl_max(int v)
+{
+    DPP_STEP(v, 0x111, 0xf);
+    DPP_STEP(v, 0x112, 0xf);
+    DPP_STEP(v, 0x114, 0xf);
+    DPP_STEP(v, 0x118, 0xf);
+    DPP_STEP(v, 0x142, 0xa);
+    DPP_STEP(v, 0x143, 0xc);
+    return __builtin_amdgcn_update_dpp(NEG_SCAN, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+}
+
+// lane l receives v of lane l-1; lane 0 receives `first`
+DEV int wave_shr1(int v, int first) { return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false); }
+
+DEV int wave_sum(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ksw_global2 over accessor-defined sequences.  eh: LDS, qlen+1 entries.  z: LDS (n_col*tlen bytes)
+// or nullptr (score only).  CIGAR (traceback) written to cig[] with libbwa push_cigar semantics.
+DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                      int e_ins, int w, int2 *eh, uint8_t *z, int zcap, uint32_t *cig, int cap, int *ncig, bool &ovf,
+                      uint64_t &cells)
+{
+    const int l = lane_id();
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    if (z && (int64_t)n_col * tlen > zcap) { ovf = true; return 0; }
+    for (int j = l; j <= qlen; j += 64)
+        eh[j] = j == 0 ? make_int2(0, MINUS_INF_W) : (j <= w ? make_int2(-(o_ins + e_ins * j), MINUS_INF_W)
+                                                             : make_int2(MINUS_INF_W, MINUS_INF_W));
+    lds_fence();
+    for (int i = 0; i < tlen; ++i) {
+        const int tb = target(i);
+        const int beg = i > w ? i - w : 0;
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        int h_carry = beg == 0 ? -(o_del + e_del * (i + 1)) : MINUS_INF_W;
+        int f_carry = MINUS_INF_W;
+        cells += (uint64_t)(end > beg ? end - beg : 0);
+        for (int c0 = beg; c0 < end; c0 += 64) {
+            const int j = c0 + l;
+            const bool act = j < end;
+            int2 p = act ? eh[j] : make_int2(0, 0);
+            const int m = p.x + (act ? mat_sc(o, tb, query(j)) : 0);
+            const int e = p.y;
+            const int tf = m - oe_ins;
+            const int g = act ? tf + l * e_ins : NEG_SCAN;
+            const int ex = wave_excl_max(g);
+            int f = f_carry - l * e_ins;
+            if (l > 0) {
+                const int fs = ex - (l - 1) * e_ins;
+                f = f > fs ? f : fs;
+            }
+            int d = m >= e ? 0 : 1;
+            int h = m >= e ? m : e;
+            d = h >= f ? d : 2;
+            h = h >= f ? h : f;
+            const int te = m - oe_del, e2 = e - e_del;
+            d |= e2 > te ? 1 << 2 : 0;
+            const int enew = e2 > te ? e2 : te;
+            const int f2 = f - e_ins;
+            d |= f2 > tf ? 2 << 4 : 0;
+            const int fnext = f2 > tf ? f2 : tf;
+            const int hprev = wave_shr1(h, h_carry);
+            if (act) {
+                eh[j] = make_int2(hprev, enew);
+                if (z) z[i * n_col + (j - beg)] = (uint8_t)d;
+            }
+            const int last = (end - 1 - c0) < 63 ? (end - 1 - c0) : 63;
+            h_carry = __builtin_amdgcn_readlane(h, last);
+            f_carry = __builtin_amdgcn_readlane(fnext, last);
+        }
+        if (l == 0) eh[end] = make_int2(h_carry, MINUS_INF_W);
+        lds_fence();
+    }
+    const int score = eh[qlen].x;
+    if (z) {
+        int n = 0, which = 0, i = tlen - 1;
+        int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+        uint32_t cur = 0;   // pending op (len<<4|op), flushed on op change
+        auto push = [&](int op, int len) {
+            if (n > 0 && (int)(cur & 0xf) == op) { cur += (uint32_t)len << 4; return; }
+            if (n > 0) {
+                if (n - 1 >= cap) { ovf = true; return; }
+                cig[n - 1] = cur;
+            }
+            cur = (uint32_t)len << 4 | (uint32_t)op;
+            ++n;
+        };
+        while (i >= 0 && k >= 0 && !ovf) {
+            which = z[i * n_col + (k - (i > w ? i - w : 0))] >> (which << 1) & 3;
+            if (which == 0) push(0, 1), --i, --k;
+            else if (which == 1) push(2, 1), --i;
+            else push(1, 1), --k;
+        }
+        if (i >= 0) push(2, i + 1);
+        if (k >= 0) push(1, k + 1);
+        if (n > cap) ovf = true;
+        if (!ovf && n > 0) cig[n - 1] = cur;
+        if (!ovf)
+            for (int a = 0; a < (n >> 1); ++a) { uint32_t t = cig[a]; cig[a] = cig[n - 1 - a]; cig[n - 1 - a] = t; }
+        *ncig = ovf ? -1 : n;
+    }
+    return score;
+}
+
+// bwa_gen_cigar2, wave version
+DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
+                     int64_t re, int *score, int2 *eh, uint8_t *z, int zcap, uint32_t *cig, int cap, int *ncig,
+                     bool &ovf, uint64_t &cells, uint64_t &bases)
+{
+    *ncig = 0;
+    if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
+    const int64_t rlen = re - rb;
+    if (re > (ix.l_pac << 1) || rb < 0) return 0;
+    bases += (uint64_t)((rlen + 3) >> 2);
+    const bool rev = rb >= ix.l_pac;
+    QAcc qa{q, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
+    TAcc ta{&ix, rev ? re - 1 : rb, rev ? -1 : 1};
+    if (l_query == rlen && w_ == 0) {
+        if (cap < 1) { ovf = true; return 0; }
+        cig[0] = (uint32_t)l_query << 4;
+        *ncig = 1;
+        int s = 0;
+        for (int i = lane_id(); i < l_query; i += 64) s += mat_sc(o, ta(i), qa(i));
+        *score = wave_sum(s);
+    } else {
+        int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
+        int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+        int max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
+        int w = (max_gap + dl + 1) >> 1;
+        w = w < w_ ? w : w_;
+        const int min_w = dl + 3;
+        w = w > min_w ? w : min_w;
+        *score = ksw_global2_w(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, z, zcap, cig,
+                               cap, ncig, ovf, cells);
+    }
+    return 1;
+}
+
+// mem_reg2aln per region, one wave per read.  LDS per wave: eh (max_len+2 int2) + z (zcap bytes).
+__global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
+                                                   const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs,
+                                                   Hit *hits, uint32_t *cigars, int32_t *n_cig_read, uint32_t *status,
+                                                   Counters *ctr, int zcap, uint8_t *zslab, int64_t zslab_bytes)
+{
+    extern __shared__ uint8_t lds_raw[];
+    const int wave = threadIdx.x >> 6;
+    const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
+    uint8_t *mine = lds_raw + (size_t)wave * (eh_bytes + (size_t)zcap);
+    int2 *eh = reinterpret_cast<int2 *>(mine);
+    uint8_t *z_lds = mine + eh_bytes;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + wave, nw = gridDim.x * (blockDim.x >> 6);
+    uint8_t *z_glob = zslab + (size_t)gw * (size_t)zslab_bytes;   // this wave's spill slab
+    uint64_t cells = 0, bases = 0;
+    for (int li = gw; li < n; li += nw) {
+    if (status[li]) { n_cig_read[li] = 0; continue; }
+    {
+        const uint8_t *q = codes + offs[li];
+        const int l_query = (int)(offs[li + 1] - offs[li]);
+        const int nr = n_regs[li];
+        bool ovf = false;
+        int tot = 0;
+        for (int g = 0; g < nr && !ovf; ++g) {
+            const Reg ar = regs[(size_t)li * cp.regs + g];
+            uint32_t *cig = cigars + ((size_t)li * cp.regs + g) * cp.cigar;
+            const int qb = ar.qb, qe = ar.qe;
+            const int64_t rb = ar.rb, re = ar.re;
+            const int flag = ar.secondary >= 0 ? 0x100 : 0;
+            int tmp = infer_bw(qe - qb, (int)(re - rb), ar.truesc, o.a, o.o_del, o.e_del);
+            int w2 = infer_bw(qe - qb, (int)(re - rb), ar.truesc, o.a, o.o_ins, o.e_ins);
+            w2 = w2 > tmp ? w2 : tmp;
+            if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
+            int i = 0, score = 0, last_sc = -(1 << 30), ncig = 0;
+            do {
+                w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+                {   // traceback matrix in LDS when it fits, else in the wave's global slab
+                    const int lq = qe - qb;
+                    int64_t rl = re - rb;
+                    int mg = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
+                    int md = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+                    mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
+                    int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
+                    int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
+                    const int64_t need = (int64_t)(lq < 2 * ww + 1 ? lq : 2 * ww + 1) * rl;
+                    const bool in_lds = need <= zcap;
+                    gen_cigar2_w(ix, o, w2, q, qb, lq, rb, re, &score, eh, in_lds ? z_lds : z_glob,
+                                 in_lds ? zcap : (int)(zslab_bytes < 0x7fffffff ? zslab_bytes : 0x7fffffff), cig,
+                                 cp.cigar - 2, &ncig, ovf, cells, bases);
+                }
+                if (ovf) break;
+                if (score == last_sc || w2 == o.w << 2) break;
+                last_sc = score;
+                w2 <<= 1;
+            } while (++i < 3 && score < ar.truesc - o.a);
+            if (ovf) break;
+            int is_rev;
+            (void)depos(ix, rb < ix.l_pac ? rb : re - 1, is_rev);
+            if (ncig > 0) {
+                if ((cig[0] & 0xf) == 2) {
+                    --ncig;
+                    for (int t = 0; t < ncig; ++t) cig[t] = cig[t + 1];
+                } else if ((cig[ncig - 1] & 0xf) == 2) --ncig;
+            }
+            if (qb != 0 || qe != l_query) {
+                const int clip5 = is_rev ? l_query - qe : qb, clip3 = is_rev ? qb : l_query - qe;
+                if (clip5) {
+                    for (int t = ncig; t > 0; --t) cig[t] = cig[t - 1];
+                    cig[0] = (uint32_t)clip5 << 4 | 3;
+                    ++ncig;
+                }
+                if (clip3) cig[ncig++] = (uint32_t)clip3 << 4 | 3;
+            }
+            Hit h;
+            h.rb = rb; h.re = re; h.qb = qb; h.qe = qe; h.rid = ar.rid; h.score = ar.score; h.flag = flag;
+            h.is_rev = is_rev; h.n_cigar = ncig; h.pad = 0;
+            hits[(size_t)li * cp.regs + g] = h;
+            tot += ncig;
+        }
+        if (ovf) {
+            if (lane_id() == 0) status[li] |= ST_OVERFLOW;
+            n_cig_read[li] = 0;
+        } else n_cig_read[li] = tot;
+    }
+    }
+    // every lane ran the same uniform control; count once per wave
+    if (lane_id() != 0) { cells = 0; bases = 0; }
+    wave_add(&ctr[STG_REG2ALN].dp_cells, cells);
+    wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
+}
+
+hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                            const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
+                            uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
+                            uint8_t *zslab, int64_t zslab_bytes, int max_blocks)
+{
+    const int waves = 4;
+    int grid = (n + waves - 1) / waves;
+    if (grid > max_blocks) grid = max_blocks;
+    if (grid == 0) return hipSuccess;
+    const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
+    const size_t sh = (size_t)waves * (eh_bytes + (size_t)zcap);
+    hipLaunchKernelGGL(k_reg2aln_w, dim3(grid), dim3(64 * waves), sh, st, ix, o, cp, codes, offs, n, regs, n_regs, hits,
+                       cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes);
+    return hipGetLastError();
+}
+
+}  // namespace bsq
