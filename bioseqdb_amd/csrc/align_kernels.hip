@@ -653,44 +653,15 @@ struct EhL {   // offset-based so the accesses stay in the LDS address space (ds
     DEV void set(int j, int2 v) const { g_lds_eh[base + j * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
-// Sequential reader of the target bases target(i) = ref_at(start + dir*i), i = 0, 1, 2, ...: keeps the
-// current and the next 16-base pac word in registers so the per-row base never waits on memory.
-struct TStream {
-    const uint8_t *pac;
-    int64_t fp;         // forward-strand pac position of the next base
-    int fstep;          // +1 / -1 along the forward pac
-    int comp;           // 3 on the reverse strand (base = 3 - pac)
-    int64_t cur_w, max_w;
-    uint32_t cur, nxt;
-    DEV uint32_t load(int64_t w) const { return (w >= 0 && w <= max_w) ? *reinterpret_cast<const uint32_t *>(pac + 4 * w) : 0u; }
-    DEV void init(const DIndex &ix, int64_t start, int dir)
-    {
-        pac = ix.pac;
-        max_w = (ix.l_pac >> 4);
-        if (start < ix.l_pac) { fp = start; fstep = dir; comp = 0; }
-        else { fp = (ix.l_pac << 1) - 1 - start; fstep = -dir; comp = 3; }
-        cur_w = fp >> 4;
-        cur = load(cur_w);
-        nxt = load(cur_w + fstep);
-    }
-    DEV int next()
-    {
-        const int64_t w = fp >> 4;
-        if (w != cur_w) { cur = w == cur_w + fstep ? nxt : load(w); cur_w = w; nxt = load(w + fstep); }
-        const int byte = (int)((fp >> 2) & 3), sh = (int)((~fp & 3) << 1);
-        const int b = (int)((cur >> (8 * byte + sh)) & 3u);
-        fp += fstep;
-        return b ^ comp;
-    }
-};
-
-template <class EH>
-DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+template <class EH, class QA>
+DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
                      int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
                      int *_gscore, int *_max_off, EH eh, uint64_t &cells)
 {
     int i, j, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, beg, end, max, max_i, max_j, max_ins, max_del, max_ie,
         gscore, max_off;
+    if (o.exp_flags & 1) { *_qle = *_tle = *_gtle = 0; *_gscore = -1; *_max_off = 0; return h0; }
+    const Score sc = score_of(o);
     if (qlen < 0) qlen = 0;
     {   // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
         const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
@@ -726,7 +697,7 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
             int2 p = eh.get(j);
             int h, M = p.x, e = p.y;
             p.x = h1;
-            M = M ? M + mat_sc(o, tb, query(j)) : 0;
+            M = M ? M + sc(tb, query(j)) : 0;
             h = M > e ? M : e;
             h = h > f ? h : f;
             h1 = h;
@@ -778,6 +749,7 @@ DEVN int ksw_global2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
                      bool &ovf, uint64_t &cells)
 {
     int i, j, k, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, score, n_col;
+    const Score sc = score_of(o);
     n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
     if (z && (int64_t)n_col * tlen > zcap) { ovf = true; return 0; }
     eh[0] = make_int2(0, MINUS_INF);
@@ -796,7 +768,7 @@ DEVN int ksw_global2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
             int32_t h, m = p.x, e = p.y;
             uint8_t d;
             p.x = h1;
-            m += mat_sc(o, tb, query(j));
+            m += sc(tb, query(j));
             d = m >= e ? 0 : 1;
             h = m >= e ? m : e;
             d = h >= f ? d : 2;
@@ -914,9 +886,23 @@ struct ExtCtx {
     bool ovf;
 };
 
-template <class EH>
+struct QMakeG {   // query accessors over the read in global memory
+    const uint8_t *q;
+    DEV QAcc at(int start, int dir) const { return QAcc{q, start, dir}; }
+};
+extern __shared__ uint8_t g_lds_q8[];   // same dynamic LDS as g_lds_eh; query bytes start at `off`
+struct QLane {   // lane-interleaved query bytes in LDS: base j of this lane at off + j*64 + lane
+    int off, start, dir;
+    DEV int operator()(int j) const { return g_lds_q8[off + (start + dir * j) * 64]; }
+};
+struct QMakeL {
+    int off;   // byte offset of this lane's column 0
+    DEV QLane at(int start, int dir) const { return QLane{off, start, dir}; }
+};
+
+template <class EH, class QM>
 DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
-                   ExtCtx &X, EH ehx, uint64_t &cells, uint64_t &bases)
+                   ExtCtx &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
 {
     int64_t l_pac = ix.l_pac, rmax0, rmax1;
     if (c.n == 0) return;
@@ -989,7 +975,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
         if (s.qbeg) {
             int qle, tle, gtle, gscore;
             int64_t tmp = s.rbeg - rmax0;
-            QAcc qa{q, s.qbeg - 1, -1};
+            auto qa = qm.at(s.qbeg - 1, -1);
             TAcc ta{&ix, s.rbeg - 1, -1};
             for (int t = 0; t < 2; ++t) {
                 int prev = a.score;
@@ -1010,7 +996,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
             int qle, tle, gtle, gscore, sc0 = a.score;
             int qe = s.qbeg + s.len;
             int re = (int)(s.rbeg + s.len - rmax0);
-            QAcc qa{q, qe, 1};
+            auto qa = qm.at(qe, 1);
             TAcc ta{&ix, rmax0 + re, 1};
             for (int t = 0; t < 2; ++t) {
                 int prev = a.score;
@@ -1188,10 +1174,14 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
         const int nc = n_chains[li];
         if (LDS) {
             EhL ehx{(int)threadIdx.x};   // blockDim == 64: lane-interleaved u16 pairs
-            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, cells, bases);
+            const int qoff = 64 * (cp.max_len + 2) * 4 + (int)threadIdx.x;
+            for (int j = 0; j < len; ++j) g_lds_q8[qoff + j * 64] = q[j];   // stage the read in LDS
+            QMakeL qm{qoff};
+            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
         } else {
             EhG ehx{X.eh};
-            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, cells, bases);
+            QMakeG qm{q};
+            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
         }
         if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
         X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
@@ -1373,7 +1363,7 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
     const bool lds = cp.max_len <= 200 && (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
-        const size_t sh = (size_t)64 * (cp.max_len + 2) * 4;
+        const size_t sh = (size_t)64 * (cp.max_len + 2) * 4 + (size_t)64 * (cp.max_len + 2);
         hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
                            seeds, n_chains, regs, n_regs, status, scratch, ctr);
     } else {

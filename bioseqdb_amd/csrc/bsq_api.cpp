@@ -331,6 +331,7 @@ DOpts make_dopts(const bsq_opts &o)
     d.max_mem_intv = 20; d.split_factor = 1.5f; d.mask_level = 0.50f; d.drop_ratio = 0.50f; d.mask_level_redun = 0.95f;
     // mem_opt_init fills mat with a=1, b=4 and bioseqdb never refills it (Q2)
     d.mat_match = 1; d.mat_mismatch = -4; d.mat_amb = -1; d.mat_max = 1;
+    { const char *e = getenv("BSQ_EXP"); d.exp_flags = e ? atoi(e) : 0; }   // timing experiments only
     return d;
 }
 
@@ -518,7 +519,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (!sel && w.cp.max_len <= 1024) {
         // main pass: one wave per read, DP rows across lanes, eh + traceback in LDS (dp_wave.hip)
         const size_t eh_bytes = ((size_t)(w.cp.max_len + 2) * 8 + 15) & ~(size_t)15;
-        const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes) & ~15;
+        const int64_t q_bytes = ((int64_t)w.cp.max_len + 16) & ~15LL;
+        const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes - q_bytes) & ~15;
         // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
         HIPCHK(launch_reg2aln_w(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
                                 w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks));

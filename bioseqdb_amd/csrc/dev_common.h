@@ -74,6 +74,19 @@ struct TAcc {   // target[i] = ref_at(start + dir*i)
     DEV int operator()(int i) const { return ref_at(*ix, start + (int64_t)dir * i); }
 };
 
+// substitution scores of bwa_fill_scmat's matrix, held in registers by the DP loops
+struct Score {
+    int match, mis, amb;
+    // bitmask selects: a ?: chain here gets turned into an indexed load from a private (scratch) table
+    DEV int operator()(int t, int q) const
+    {
+        const int eq = -(int)(t == q), nn = -(int)((t | q) >= 4);
+        const int r = (match & eq) | (mis & ~eq);
+        return (amb & nn) | (r & ~nn);
+    }
+};
+DEV Score score_of(const DOpts &o) { Score s; s.match = o.mat_match; s.mis = o.mat_mismatch; s.amb = o.mat_amb; return s; }
+
 DEV int mat_sc(const DOpts &o, int t, int q)
 {
     return (t == 4 || q == 4) ? o.mat_amb : (t == q ? o.mat_match : o.mat_mismatch);
@@ -89,5 +102,36 @@ DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
     return w;
 }
 
+
+// Sequential reader of the target bases target(i) = ref_at(start + dir*i), i = 0, 1, 2, ...: keeps the
+// current and the next 16-base pac word in registers so the per-row base never waits on memory.
+struct TStream {
+    const uint8_t *pac;
+    int64_t fp;         // forward-strand pac position of the next base
+    int fstep;          // +1 / -1 along the forward pac
+    int comp;           // 3 on the reverse strand (base = 3 - pac)
+    int64_t cur_w, max_w;
+    uint32_t cur, nxt;
+    DEV uint32_t load(int64_t w) const { return (w >= 0 && w <= max_w) ? *reinterpret_cast<const uint32_t *>(pac + 4 * w) : 0u; }
+    DEV void init(const DIndex &ix, int64_t start, int dir)
+    {
+        pac = ix.pac;
+        max_w = (ix.l_pac >> 4);
+        if (start < ix.l_pac) { fp = start; fstep = dir; comp = 0; }
+        else { fp = (ix.l_pac << 1) - 1 - start; fstep = -dir; comp = 3; }
+        cur_w = fp >> 4;
+        cur = load(cur_w);
+        nxt = load(cur_w + fstep);
+    }
+    DEV int next()
+    {
+        const int64_t w = fp >> 4;
+        if (w != cur_w) { cur = w == cur_w + fstep ? nxt : load(w); cur_w = w; nxt = load(w + fstep); }
+        const int byte = (int)((fp >> 2) & 3), sh = (int)((~fp & 3) << 1);
+        const int b = (int)((cur >> (8 * byte + sh)) & 3u);
+        fp += fstep;
+        return b ^ comp;
+    }
+};
 
 }  // namespace bsq

@@ -51,11 +51,19 @@ DEV int wave_sum(int v)
 
 // ksw_global2 over accessor-defined sequences.  eh: LDS, qlen+1 entries.  z: LDS (n_col*tlen bytes)
 // or nullptr (score only).  CIGAR (traceback) written to cig[] with libbwa push_cigar semantics.
-DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+extern __shared__ uint8_t g_lds_dp[];   // dynamic LDS of k_reg2aln_w
+struct QW {   // query bases staged in this wave's LDS: base j at off + start + dir*j
+    int off, start, dir;
+    DEV int operator()(int j) const { return g_lds_dp[off + start + dir * j]; }
+};
+
+template <class QA>
+DEV int ksw_global2_w(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
                       int e_ins, int w, int2 *eh, uint8_t *z, int zcap, uint32_t *cig, int cap, int *ncig, bool &ovf,
                       uint64_t &cells)
 {
     const int l = lane_id();
+    const Score sc = score_of(o);
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
     const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
     if (z && (int64_t)n_col * tlen > zcap) { ovf = true; return 0; }
@@ -63,8 +71,10 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc targe
         eh[j] = j == 0 ? make_int2(0, MINUS_INF_W) : (j <= w ? make_int2(-(o_ins + e_ins * j), MINUS_INF_W)
                                                              : make_int2(MINUS_INF_W, MINUS_INF_W));
     lds_fence();
-    for (int i = 0; i < tlen; ++i) {
-        const int tb = target(i);
+    TStream ts;
+    if (tlen > 0) ts.init(*target.ix, target.start, target.dir);
+    for (int i = 0; i < ((o.exp_flags & 4) ? 0 : tlen); ++i) {
+        const int tb = ts.next();   // uniform; next pac word prefetched
         const int beg = i > w ? i - w : 0;
         const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
         int h_carry = beg == 0 ? -(o_del + e_del * (i + 1)) : MINUS_INF_W;
@@ -74,7 +84,7 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc targe
             const int j = c0 + l;
             const bool act = j < end;
             int2 p = act ? eh[j] : make_int2(0, 0);
-            const int m = p.x + (act ? mat_sc(o, tb, query(j)) : 0);
+            const int m = p.x + (act ? sc(tb, query(j)) : 0);
             const int e = p.y;
             const int tf = m - oe_ins;
             const int g = act ? tf + l * e_ins : NEG_SCAN;
@@ -107,6 +117,7 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc targe
         lds_fence();
     }
     const int score = eh[qlen].x;
+    if (z && (o.exp_flags & 2)) { cig[0] = (uint32_t)qlen << 4; *ncig = 1; return score; }
     if (z) {
         int n = 0, which = 0, i = tlen - 1;
         int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
@@ -137,10 +148,105 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QAcc query, int tlen, TAcc targe
     return score;
 }
 
+// lane l receives v of lane l+1; the last lane receives `last`
+DEV int wave_shl1(int v, int last) { return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false); }
+
+// ksw_global2 for bands of at most 64 columns with the row state held in registers.  In global mode the
+// band is [max(0,i-w), min(i+w+1,qlen)): it slides by s = 0 or 1 column per row and grows by one at the
+// right, and the column entering at the right reads (H(i-1,end-1), -inf), so the next row's state is
+//   s == 0: Hd' = h of lane l-1 (lane 0: the column-0 boundary value), E' = e_new of lane l
+//   s == 1: Hd' = h of lane l,                                        E' = e_new of lane l+1
+// (-inf for the new column's E) -- exactly the eh[] values the serial kernel would read.
+template <bool ZL>
+DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_dir, TStream ts, int tlen, int o_del,
+                        int e_del, int o_ins, int e_ins, int w, int n_col, int z_off, uint8_t *zg, uint64_t &cells)
+{
+    const int l = lane_id();
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    int Hd = l == 0 ? 0 : (l <= w ? -(o_ins + e_ins * l) : MINUS_INF_W);
+    int E = MINUS_INF_W;
+    int beg = 0, last_end = 0, h_last = 0;
+    for (int i = 0; i < tlen; ++i) {
+        const int tb = ts.next();
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        const int width = end - beg;
+        const bool act = l < width;
+        const int j = beg + l;
+        const int qv = act ? g_lds_dp[q_off + q_start + q_dir * j] : 0;
+        const int m = Hd + sc(tb, qv);
+        const int tf = m - oe_ins;
+        const int ex = wave_excl_max(act ? tf + l * e_ins : NEG_SCAN);
+        int f = MINUS_INF_W - l * e_ins;
+        if (l > 0) { const int fs = ex - (l - 1) * e_ins; f = f > fs ? f : fs; }
+        int d = m >= E ? 0 : 1;
+        int h = m >= E ? m : E;
+        d = h >= f ? d : 2;
+        h = h >= f ? h : f;
+        const int te = m - oe_del, e2 = E - e_del;
+        d |= e2 > te ? 1 << 2 : 0;
+        const int enew = e2 > te ? e2 : te;
+        const int f2 = f - e_ins;
+        d |= f2 > tf ? 2 << 4 : 0;
+        if (act) {
+            if (ZL) g_lds_dp[z_off + i * n_col + l] = (uint8_t)d;
+            else zg[i * n_col + l] = (uint8_t)d;
+        }
+        cells += (uint64_t)width;
+        h_last = __builtin_amdgcn_readlane(h, width - 1);
+        last_end = end;
+        const int beg_next = i + 1 > w ? i + 1 - w : 0;
+        if (beg_next == beg) {
+            Hd = wave_shr1(h, -(o_del + e_del * (i + 1)));
+            E = l < width ? enew : MINUS_INF_W;
+        } else {
+            Hd = h;
+            const int es = wave_shl1(enew, MINUS_INF_W);
+            E = l + 1 < width ? es : MINUS_INF_W;
+        }
+        beg = beg_next;
+    }
+    if (last_end == qlen) return h_last;
+    return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
+}
+
+// traceback of a z matrix held in LDS (offset) or global memory; libbwa push_cigar semantics
+template <bool ZL>
+DEV void traceback_w(int qlen, int tlen, int w, int n_col, int z_off, const uint8_t *zg, uint32_t *cig, int cap,
+                     int *ncig, bool &ovf)
+{
+    int n = 0, which = 0, i = tlen - 1;
+    int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+    uint32_t cur = 0;
+    auto push = [&](int op, int len) {
+        if (n > 0 && (int)(cur & 0xf) == op) { cur += (uint32_t)len << 4; return; }
+        if (n > 0) {
+            if (n - 1 >= cap) { ovf = true; return; }
+            cig[n - 1] = cur;
+        }
+        cur = (uint32_t)len << 4 | (uint32_t)op;
+        ++n;
+    };
+    while (i >= 0 && k >= 0 && !ovf) {
+        const int idx = i * n_col + (k - (i > w ? i - w : 0));
+        const int zz = ZL ? g_lds_dp[z_off + idx] : zg[idx];
+        which = zz >> (which << 1) & 3;
+        if (which == 0) push(0, 1), --i, --k;
+        else if (which == 1) push(2, 1), --i;
+        else push(1, 1), --k;
+    }
+    if (i >= 0) push(2, i + 1);
+    if (k >= 0) push(1, k + 1);
+    if (n > cap) ovf = true;
+    if (!ovf && n > 0) cig[n - 1] = cur;
+    if (!ovf)
+        for (int a = 0; a < (n >> 1); ++a) { uint32_t t = cig[a]; cig[a] = cig[n - 1 - a]; cig[n - 1 - a] = t; }
+    *ncig = ovf ? -1 : n;
+}
+
 // bwa_gen_cigar2, wave version
-DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
-                     int64_t re, int *score, int2 *eh, uint8_t *z, int zcap, uint32_t *cig, int cap, int *ncig,
-                     bool &ovf, uint64_t &cells, uint64_t &bases)
+DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb, int l_query, int64_t rb,
+                     int64_t re, int *score, int2 *eh, uint8_t *z, int z_off, int zcap, uint32_t *cig, int cap,
+                     int *ncig, bool &ovf, uint64_t &cells, uint64_t &bases)
 {
     *ncig = 0;
     if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
@@ -148,14 +254,15 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q,
     if (re > (ix.l_pac << 1) || rb < 0) return 0;
     bases += (uint64_t)((rlen + 3) >> 2);
     const bool rev = rb >= ix.l_pac;
-    QAcc qa{q, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
+    QW qa{q_off, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
     TAcc ta{&ix, rev ? re - 1 : rb, rev ? -1 : 1};
     if (l_query == rlen && w_ == 0) {
         if (cap < 1) { ovf = true; return 0; }
         cig[0] = (uint32_t)l_query << 4;
         *ncig = 1;
         int s = 0;
-        for (int i = lane_id(); i < l_query; i += 64) s += mat_sc(o, ta(i), qa(i));
+        const Score sc = score_of(o);
+        for (int i = lane_id(); i < l_query; i += 64) s += sc(ta(i), qa(i));
         *score = wave_sum(s);
     } else {
         int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
@@ -167,8 +274,24 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q,
         w = w < w_ ? w : w_;
         const int min_w = dl + 3;
         w = w > min_w ? w : min_w;
-        *score = ksw_global2_w(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, z, zcap, cig,
-                               cap, ncig, ovf, cells);
+        const int n_col = l_query < 2 * w + 1 ? l_query : 2 * w + 1;
+        if (n_col <= 64 && rlen < (int64_t)l_query + w && !(o.exp_flags & 4)) {
+            // register-resident rows; traceback matrix in LDS (z_off >= 0) or the global slab
+            if ((int64_t)n_col * rlen > zcap) { ovf = true; return 0; }
+            TStream ts;
+            ts.init(ix, ta.start, ta.dir);
+            const bool zl = z_off >= 0;
+            *score = zl ? ksw_global2_reg<true>(score_of(o), l_query, q_off, qa.start, qa.dir, ts, (int)rlen, o.o_del,
+                                                o.e_del, o.o_ins, o.e_ins, w, n_col, z_off, nullptr, cells)
+                        : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ts, (int)rlen, o.o_del,
+                                                 o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
+            if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
+            if (zl) traceback_w<true>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
+            else traceback_w<false>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
+        } else {
+            *score = ksw_global2_w(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, z, zcap,
+                                   cig, cap, ncig, ovf, cells);
+        }
     }
     return 1;
 }
@@ -179,12 +302,14 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
                                                    Hit *hits, uint32_t *cigars, int32_t *n_cig_read, uint32_t *status,
                                                    Counters *ctr, int zcap, uint8_t *zslab, int64_t zslab_bytes)
 {
-    extern __shared__ uint8_t lds_raw[];
     const int wave = threadIdx.x >> 6;
     const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
-    uint8_t *mine = lds_raw + (size_t)wave * (eh_bytes + (size_t)zcap);
+    const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
+    const size_t per_wave = eh_bytes + (size_t)zcap + q_bytes;
+    uint8_t *mine = g_lds_dp + (size_t)wave * per_wave;
     int2 *eh = reinterpret_cast<int2 *>(mine);
     uint8_t *z_lds = mine + eh_bytes;
+    const int q_off = (int)((size_t)wave * per_wave + eh_bytes + (size_t)zcap);
     const int gw = blockIdx.x * (blockDim.x >> 6) + wave, nw = gridDim.x * (blockDim.x >> 6);
     uint8_t *z_glob = zslab + (size_t)gw * (size_t)zslab_bytes;   // this wave's spill slab
     uint64_t cells = 0, bases = 0;
@@ -194,6 +319,8 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
         const uint8_t *q = codes + offs[li];
         const int l_query = (int)(offs[li + 1] - offs[li]);
         const int nr = n_regs[li];
+        for (int j = lane_id(); j < l_query; j += 64) g_lds_dp[q_off + j] = q[j];   // stage the read
+        lds_fence();
         bool ovf = false;
         int tot = 0;
         for (int g = 0; g < nr && !ovf; ++g) {
@@ -219,7 +346,8 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
                     int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
                     const int64_t need = (int64_t)(lq < 2 * ww + 1 ? lq : 2 * ww + 1) * rl;
                     const bool in_lds = need <= zcap;
-                    gen_cigar2_w(ix, o, w2, q, qb, lq, rb, re, &score, eh, in_lds ? z_lds : z_glob,
+                    gen_cigar2_w(ix, o, w2, q_off, qb, lq, rb, re, &score, eh, in_lds ? z_lds : z_glob,
+                                 in_lds ? (int)((size_t)wave * per_wave + eh_bytes) : -1,
                                  in_lds ? zcap : (int)(zslab_bytes < 0x7fffffff ? zslab_bytes : 0x7fffffff), cig,
                                  cp.cigar - 2, &ncig, ovf, cells, bases);
                 }
@@ -274,7 +402,8 @@ hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, co
     if (grid > max_blocks) grid = max_blocks;
     if (grid == 0) return hipSuccess;
     const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
-    const size_t sh = (size_t)waves * (eh_bytes + (size_t)zcap);
+    const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
+    const size_t sh = (size_t)waves * (eh_bytes + (size_t)zcap + q_bytes);
     hipLaunchKernelGGL(k_reg2aln_w, dim3(grid), dim3(64 * waves), sh, st, ix, o, cp, codes, offs, n, regs, n_regs, hits,
                        cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes);
     return hipGetLastError();
