@@ -45,6 +45,8 @@ hipError_t launch_reg2aln_w(hipStream_t, const DIndex &, const DOpts &, const Ca
                             uint8_t *, int64_t, int);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int);
+hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                            int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 }  // namespace bsq
 
 using namespace bsq;
@@ -505,7 +507,13 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         const int lcap = tiny_caps() ? 3 : ix.seq_len < 0xFFFFFFFFull ? 28 : 16;
-        HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap));
+        static const char *alt = getenv("BSQ_SMEM");
+        static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
+        if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)
+            HIPCHK(launch_smem_flat(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap,
+                                    sblocks));
+        else
+            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap));
     } else {
         HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }

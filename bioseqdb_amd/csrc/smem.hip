@@ -27,54 +27,90 @@ struct FM {
     DEV X L2(int c) const { return c == 0 ? l2_0 : c == 1 ? l2_1 : c == 2 ? l2_2 : c == 3 ? l2_3 : l2_4; }
 };
 
+// rank of base c and of all bases > c in rows [0, k] (k = -1 -> 0), from a loaded occ block: the two
+// sums bwt_extend needs for one base.  Selection is by bit masks so every word of the block is used
+// unconditionally (a select chain lets the compiler narrow the block load and sink parts of it into
+// branches, serialising the two blocks' round trips).
 template <typename X>
-DEV void occ4x(const FM<X> &fm, X k, X c[4])
+DEV void occ_c(const uint4 (&w)[4], X k, bool none, int c, X &cc, X &cg)
 {
-    if (k == (X)-1) { c[0] = c[1] = c[2] = c[3] = 0; return; }
-    k -= (k >= fm.primary);
-    const uint4 *p = reinterpret_cast<const uint4 *>(fm.occ + (k >> 7));
-    uint4 w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3];
     const uint32_t r = (uint32_t)(k & 127) + 1;
-    uint64_t h0 = (uint64_t)w2.y << 32 | w2.x, h1 = (uint64_t)w2.w << 32 | w2.z;
-    uint64_t l0 = (uint64_t)w3.y << 32 | w3.x, l1 = (uint64_t)w3.w << 32 | w3.z;
-    uint64_t m0 = r >= 64 ? ~0ull : ((1ull << r) - 1);
-    uint64_t m1 = r >= 128 ? ~0ull : (r > 64 ? ((1ull << (r - 64)) - 1) : 0ull);
-    uint32_t n3 = __popcll(h0 & l0 & m0) + __popcll(h1 & l1 & m1);
-    uint32_t n2 = __popcll(h0 & ~l0 & m0) + __popcll(h1 & ~l1 & m1);
-    uint32_t n1 = __popcll(~h0 & l0 & m0) + __popcll(~h1 & l1 & m1);
+    const uint64_t h0 = (uint64_t)w[2].y << 32 | w[2].x, h1 = (uint64_t)w[2].w << 32 | w[2].z;
+    const uint64_t l0 = (uint64_t)w[3].y << 32 | w[3].x, l1 = (uint64_t)w[3].w << 32 | w[3].z;
+    const uint64_t m0 = r >= 64 ? ~0ull : ((1ull << r) - 1);
+    const uint64_t m1 = r >= 128 ? ~0ull : (r > 64 ? ((1ull << (r - 64)) - 1) : 0ull);
+    // base b is (h, l) = (b >> 1, b & 1): plane of c, and plane of bases > c
+    const uint64_t fh = (c & 2) ? 0ull : ~0ull, fl = (c & 1) ? 0ull : ~0ull;
+    const uint64_t any = c == 0 ? ~0ull : 0ull;
+    const uint64_t ah0 = c < 2 ? ~0ull : (c == 2 ? l0 : 0ull), ah1 = c < 2 ? ~0ull : (c == 2 ? l1 : 0ull);
+    const uint32_t nc = __popcll((h0 ^ fh) & (l0 ^ fl) & m0) + __popcll((h1 ^ fh) & (l1 ^ fl) & m1);
+    const uint32_t ng = __popcll(((h0 & ah0) | (l0 & any)) & m0) + __popcll(((h1 & ah1) | (l1 & any)) & m1);
+    X b0, b1, b2, b3;
     if (sizeof(X) == 4) {
-        c[0] = (X)w0.x + (r - n1 - n2 - n3);
-        c[1] = (X)w0.z + n1;
-        c[2] = (X)w1.x + n2;
-        c[3] = (X)w1.z + n3;
+        b0 = (X)w[0].x; b1 = (X)w[0].z; b2 = (X)w[1].x; b3 = (X)w[1].z;
     } else {
-        c[0] = (X)((uint64_t)w0.y << 32 | w0.x) + (r - n1 - n2 - n3);
-        c[1] = (X)((uint64_t)w0.w << 32 | w0.z) + n1;
-        c[2] = (X)((uint64_t)w1.y << 32 | w1.x) + n2;
-        c[3] = (X)((uint64_t)w1.w << 32 | w1.z) + n3;
+        b0 = (X)((uint64_t)w[0].y << 32 | w[0].x); b1 = (X)((uint64_t)w[0].w << 32 | w[0].z);
+        b2 = (X)((uint64_t)w[1].y << 32 | w[1].x); b3 = (X)((uint64_t)w[1].w << 32 | w[1].z);
     }
+    const X live = none ? (X)0 : ~(X)0;
+    const X s0 = -(X)(c == 0), s1 = -(X)(c == 1), s2 = -(X)(c == 2), s3 = -(X)(c == 3);
+    cc = (((b0 & s0) | (b1 & s1) | (b2 & s2) | (b3 & s3)) + nc) & live;
+    cg = ((b1 & s0) + (b2 & (s0 | s1)) + (b3 & (s0 | s1 | s2)) + ng) & live;
 }
-
-template <typename X>
-DEV X pick(const X v[4], int c) { return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3]; }
 
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
 // used for the rank queries (x[1] forward, x[0] backward), `o` the other one.
 template <typename X>
 DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, uint64_t &nblk)
 {
-    X tk[4], tl[4];
     const X k = a - 1, l = a - 1 + x2;
-    occ4x(fm, k, tk);
-    occ4x(fm, l, tl);
-    {
-        X kk = k == (X)-1 ? k : k - (k >= fm.primary), ll = l - (l >= fm.primary);
-        nblk += (k == (X)-1 || (kk >> 7) == (ll >> 7)) ? 1 : 2;
-    }
-    const X d3 = tl[3] - tk[3], d2 = tl[2] - tk[2], d1 = tl[1] - tk[1];
-    na = fm.L2(c) + 1 + pick(tk, c);
-    nx2 = pick(tl, c) - pick(tk, c);
-    no = o + (X)(a <= fm.primary && a + x2 - 1 >= fm.primary) + (c < 3 ? d3 : 0) + (c < 2 ? d2 : 0) + (c < 1 ? d1 : 0);
+    const bool knone = k == (X)-1;
+    const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
+    const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ + (knone ? 0 : (kk >> 7)));
+    const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ + (ll >> 7));
+    uint4 wk[4], wl[4];
+    wk[0] = pk[0]; wk[1] = pk[1]; wk[2] = pk[2]; wk[3] = pk[3];
+    wl[0] = pl[0]; wl[1] = pl[1]; wl[2] = pl[2]; wl[3] = pl[3];
+    X kc, kg, lc, lg;
+    occ_c(wk, kk, knone, c, kc, kg);
+    occ_c(wl, ll, false, c, lc, lg);
+    nblk += (knone || (kk >> 7) == (ll >> 7)) ? 1 : 2;
+    na = fm.L2(c) + 1 + kc;
+    nx2 = lc - kc;
+    no = o + (X)(a <= fm.primary && a + x2 - 1 >= fm.primary) + (lg - kg);
+}
+
+// Two independent backward extensions by the same base (entries of one bwt_smem1 backward level);
+// all four occ blocks are in flight together.  Backward extensions only need (x[0], x[2]).
+template <typename X>
+DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool hb, int c, X &ra0, X &ra2, X &rb0, X &rb2,
+                   uint64_t &nblk)
+{
+    const X ka = a0 - 1, la = a0 - 1 + a2;
+    const X kb = hb ? b0 - 1 : ka, lb = hb ? b0 - 1 + b2 : la;
+    const bool kan = ka == (X)-1, kbn = kb == (X)-1;
+    const X kka = ka - (ka >= fm.primary), lla = la - (la >= fm.primary);
+    const X kkb = kb - (kb >= fm.primary), llb = lb - (lb >= fm.primary);
+    const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ + (kan ? 0 : (kka >> 7)));
+    const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ + (lla >> 7));
+    const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ + (kbn ? 0 : (kkb >> 7)));
+    const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ + (llb >> 7));
+    uint4 w0[4], w1[4], w2[4], w3[4];
+    w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
+    w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
+    w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
+    w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
+    X kc, kg, lc, lg;
+    occ_c(w0, kka, kan, c, kc, kg);
+    occ_c(w1, lla, false, c, lc, lg);
+    ra0 = fm.L2(c) + 1 + kc;
+    ra2 = lc - kc;
+    occ_c(w2, kkb, kbn, c, kc, kg);
+    occ_c(w3, llb, false, c, lc, lg);
+    rb0 = fm.L2(c) + 1 + kc;
+    rb2 = lc - kc;
+    nblk += (kan || (kka >> 7) == (lla >> 7)) ? 1 : 2;
+    if (hb) nblk += (kbn || (kkb >> 7) == (llb >> 7)) ? 1 : 2;
 }
 
 // LDS list of (x0, x2, end) entries for one lane: entry e at base[e * stride]
@@ -139,27 +175,35 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         int nc = 0;
         X last_x2 = 0;
-        for (int j = 0; j < n; ++j) {
-            const X p0 = L.x0[j * L.stride], p2 = L.x2[j * L.stride];
-            const int pe = L.end[j * L.stride];
-            bool keep_hit;
-            X o0 = 0, o1, o2 = 0;
-            if (c >= 0) {
-                extend1(fm, p0, (X)0, p2, c, o0, o1, o2, nblk);   // x[1] is dead in the backward phase
-                keep_hit = o2 < (X)min_intv;
-            } else keep_hit = true;
-            if (keep_hit) {
-                if (nc == 0 && (S.n1 == 0 || i + 1 < last_start)) {
-                    if (S.n + S.n1 >= S.cap) { ovf = true; return len; }
-                    Intv &m = S.a[S.cap - 1 - S.n1];
-                    m.x[0] = p0; m.x[1] = 0; m.x[2] = p2;
-                    m.info = (uint64_t)(uint32_t)(i + 1) << 32 | (uint32_t)pe;
-                    ++S.n1;
-                    last_start = i + 1;
+        for (int j = 0; j < n; j += 2) {
+            // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
+            // Compaction writes go to nc <= j, below both entries already read.
+            const bool hb = j + 1 < n;
+            const X pa0 = L.x0[j * L.stride], pa2 = L.x2[j * L.stride];
+            const int pae = L.end[j * L.stride];
+            const int jb = hb ? j + 1 : j;
+            const X pb0 = L.x0[jb * L.stride], pb2 = L.x2[jb * L.stride];
+            const int pbe = L.end[jb * L.stride];
+            X oa0 = 0, oa2 = 0, ob0 = 0, ob2 = 0;
+            if (c >= 0) ext_back2(fm, pa0, pa2, pb0, pb2, hb, c, oa0, oa2, ob0, ob2, nblk);
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && !hb) break;
+                const X p0 = h ? pb0 : pa0, p2 = h ? pb2 : pa2, o0 = h ? ob0 : oa0, o2 = h ? ob2 : oa2;
+                const int pe = h ? pbe : pae;
+                const bool keep_hit = c < 0 || o2 < (X)min_intv;
+                if (keep_hit) {
+                    if (nc == 0 && (S.n1 == 0 || i + 1 < last_start)) {
+                        if (S.n + S.n1 >= S.cap) { ovf = true; return len; }
+                        Intv &m = S.a[S.cap - 1 - S.n1];
+                        m.x[0] = p0; m.x[1] = 0; m.x[2] = p2;
+                        m.info = (uint64_t)(uint32_t)(i + 1) << 32 | (uint32_t)pe;
+                        ++S.n1;
+                        last_start = i + 1;
+                    }
+                } else if (nc == 0 || o2 != last_x2) {
+                    L.set(nc++, o0, o2, pe);
+                    last_x2 = o2;
                 }
-            } else if (nc == 0 || o2 != last_x2) {
-                L.set(nc++, o0, o2, pe);
-                last_x2 = o2;
             }
         }
         if (nc == 0) break;
@@ -229,10 +273,11 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
         auto take_mem1 = [&](bool pass2) {
             // mem1 (reversed emission order) sits at S.a[cap-n1 .. cap); filter-append in order
             for (int k = 0; k < S.n1; ++k) {
-                Intv m = S.a[S.cap - S.n1 + k];
-                uint32_t st = (uint32_t)(m.info >> 32), en = (uint32_t)m.info;
+                const Intv &m = S.a[S.cap - S.n1 + k];
+                const uint64_t m0 = m.x[0], m2 = m.x[2], mi = m.info;
+                uint32_t st = (uint32_t)(mi >> 32), en = (uint32_t)mi;
                 bool keep = pass2 ? (uint64_t)(en - st) >= (uint64_t)o.min_seed_len : (int)(en - st) >= o.min_seed_len;
-                if (keep) S.a[S.n++] = m;
+                if (keep) { Intv &d = S.a[S.n++]; d.x[0] = m0; d.x[1] = 0; d.x[2] = m2; d.info = mi; }
             }
             S.n1 = 0;
         };
@@ -259,7 +304,8 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
                     x = seed_strategy1_x(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk);
                     if (m.x[2] > 0) {
                         if (S.n >= S.cap) { ovf = true; break; }
-                        S.a[S.n++] = m;
+                        Intv &d = S.a[S.n++];
+                        d.x[0] = m.x[0]; d.x[1] = m.x[1]; d.x[2] = m.x[2]; d.info = m.info;
                     }
                 } else ++x;
             }
@@ -268,11 +314,17 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             status[li] |= ST_OVERFLOW;
             n_intv[li] = 0;
         } else {
-            for (int i = 1; i < S.n; ++i) {   // equal keys are identical intervals: any correct sort is exact
-                Intv tv = S.a[i];
-                int j = i;
-                while (j > 0 && tv.info < S.a[j - 1].info) { S.a[j] = S.a[j - 1]; --j; }
-                S.a[j] = tv;
+            Intv *out = S.a;
+            for (int a = 1; a < S.n; ++a) {   // equal keys are identical intervals: any correct sort is exact
+                const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
+                int b = a;
+                for (; b > 0; --b) {
+                    const uint64_t pi = out[b - 1].info;
+                    if (!(ti < pi)) break;
+                    out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
+                    out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
+                }
+                out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
             }
             n_intv[li] = S.n;
         }
@@ -298,6 +350,304 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     } else {
         size_t sh = lds_bytes<uint64_t>(T, lcap);
         hipLaunchKernelGGL(k_smem_lds<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
+                           status, ctr, lcap);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_smem_flat: the same computation as k_smem_lds restated as a per-lane state machine whose loop
+// issues exactly one bwt_extend per lane per iteration, whichever part of mem_collect_intv the lane
+// is in (smem1 forward / backward, pass 2, seed strategy), and persistent lanes: a lane that
+// finishes its read takes the next one (grid-stride), so lanes never idle behind the slowest read
+// of their wave.  Two restatements make this possible without changing the output:
+//  * the forward list is walked top-down in place instead of being reversed (logical entry j of
+//    the backward phase is physical entry top - j; the compacted list is written at top - nc,
+//    never above an entry still to be read);
+//  * mem1 is filtered straight into the output slot at emission: mem_collect_intv only appends the
+//    entries with end - start >= min_seed_len and the slot is sorted by info at the end, where equal
+//    keys are identical intervals, so the append order cannot show.
+enum : int { PH_NEXT = 0, PH_SEEK1, PH_FWD, PH_BWD, PH_SEEK2, PH_SEEKS, PH_STF, PH_FIN, PH_EXIT };
+
+template <typename X>
+__global__ void __launch_bounds__(256) k_smem_flat(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
+                                                   const int64_t *offs, int n, Intv *intv_out, int32_t *n_intv,
+                                                   uint32_t *status, Counters *ctr, int lcap)
+{
+    extern __shared__ uint8_t lds_raw[];
+    const int T = blockDim.x, t = threadIdx.x;
+    X *Lx0 = reinterpret_cast<X *>(lds_raw) + t;
+    X *Lx2 = reinterpret_cast<X *>(lds_raw) + (size_t)T * lcap + t;
+    uint16_t *Lend = reinterpret_cast<uint16_t *>(lds_raw + (size_t)2 * T * lcap * sizeof(X)) + t;
+    FM<X> fm;
+    fm.occ = ix.occ;
+    fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
+    fm.primary = (X)ix.primary;
+    const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
+    const int min_seed_len = o.min_seed_len;
+    const uint64_t split_width = (uint64_t)o.split_width;
+    const int max_mem_intv = o.max_mem_intv;
+    const int stride = gridDim.x * T;
+    uint64_t nblk = 0;
+
+    int li = blockIdx.x * T + t - stride;
+    const uint8_t *q = codes;
+    int len = 0, sn = 0, cap = cp.intv;
+    Intv *out = intv_out;
+    bool ovf = false;
+    int phase = PH_NEXT, pass = 1;
+    int x = 0, k = 0, old_n = 0;
+    int sx = 0, i = 0, ikend = 0, nl = 0, ret = 0, n1 = 0, last_start = 0, bi = 0, j = 0, nc = 0, cb = 0, top = 0;
+    int ee = 0;
+    X minI = 1, ik0 = 0, ik1 = 0, ik2 = 0, last_x2 = 0, e0 = 0, e2 = 0;
+    X ea = 0, eo = 0, ex2 = 0;
+    int ec = 0;
+    X r_new = 0, r_oth = 0, r_2 = 0;
+    bool have_res = false;
+    // one-ahead prefetch of the base the lane will need next (issued with the extend's loads)
+    int qp_pos = -1, qp_val = 0, pp = -1;
+    auto getq = [&](int pos) -> int { return pos == qp_pos ? qp_val : (int)q[pos]; };
+
+    bool want = false;
+    for (;;) {
+        // slow path: lanes without a pending request run the full machine until they have one
+        while (!want && phase != PH_EXIT) {
+            if (phase == PH_FWD || phase == PH_STF) {
+                if (have_res) {
+                    have_res = false;
+                    if (phase == PH_FWD) {
+                        if (r_2 != ik2) {
+                            if (nl >= lcap) { ovf = true; phase = PH_FIN; continue; }
+                            Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl;
+                            if (r_2 < minI) goto start_bwd;
+                        }
+                        ikend = i + 1;
+                    } else if (r_2 < (X)max_mem_intv && i - sx >= min_seed_len) {
+                        if (r_2 > 0) {
+                            if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
+                            Intv m;
+                            m.x[0] = r_oth; m.x[1] = r_new; m.x[2] = r_2;
+                            m.info = (uint64_t)sx << 32 | (uint64_t)(i + 1);
+                            out[sn++] = m;
+                        }
+                        x = i + 1; phase = PH_SEEKS; continue;
+                    }
+                    ik0 = r_oth; ik1 = r_new; ik2 = r_2; ++i;
+                }
+                {
+                    const int cur = i < len ? getq(i) : 4;
+                    if (cur < 4) {
+                        ea = ik1; eo = ik0; ex2 = ik2; ec = 3 - cur; want = true;
+                        pp = i + 1 < len ? i + 1 : -1;
+                        continue;
+                    }
+                }
+                if (phase == PH_STF) { x = i < len ? i + 1 : len; phase = PH_SEEKS; continue; }
+                // ambiguous base or end of read: push the current interval and turn backwards
+                if (nl >= lcap) { ovf = true; phase = PH_FIN; continue; }
+                Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl;
+            start_bwd:
+                top = nl - 1;
+                ret = Lend[top * T];
+                last_start = 0x7fffffff;
+                bi = sx - 1;
+                cb = bi < 0 ? -1 : (q[bi] < 4 ? q[bi] : -1);
+                j = 0; nc = 0; last_x2 = 0;
+                phase = PH_BWD;
+                continue;
+            }
+            if (phase == PH_BWD) {
+                bool hit = false;
+                if (have_res) {
+                    have_res = false;
+                    if (r_2 < minI) hit = true;
+                    else {
+                        if (nc == 0 || r_2 != last_x2) {
+                            const int p = (top - nc) * T;
+                            Lx0[p] = r_new; Lx2[p] = r_2; Lend[p] = (uint16_t)ee;
+                            ++nc; last_x2 = r_2;
+                        }
+                        ++j;
+                    }
+                } else if (j < nl) {
+                    const int p = (top - j) * T;
+                    e0 = Lx0[p]; e2 = Lx2[p]; ee = Lend[p];
+                    if (cb >= 0) { ea = e0; eo = 0; ex2 = e2; ec = cb; want = true; pp = bi - 1; continue; }
+                    hit = true;
+                } else {
+                    if (nc == 0) {   // smem1 returns
+                        if (pass == 1) { x = ret; phase = PH_SEEK1; }
+                        else { ++k; phase = PH_SEEK2; }
+                        continue;
+                    }
+                    nl = nc; --bi;
+                    cb = bi < 0 ? -1 : getq(bi);
+                    cb = cb < 4 ? cb : -1;
+                    j = 0; nc = 0; last_x2 = 0;
+                    continue;
+                }
+                if (hit) {
+                    if (nc == 0 && (n1 == 0 || bi + 1 < last_start)) {
+                        ++n1; last_start = bi + 1;
+                        if (ee - (bi + 1) >= min_seed_len) {
+                            if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
+                            Intv m;
+                            m.x[0] = e0; m.x[1] = 0; m.x[2] = e2;
+                            m.info = (uint64_t)(uint32_t)(bi + 1) << 32 | (uint32_t)ee;
+                            out[sn++] = m;
+                        }
+                    }
+                    ++j;
+                }
+                continue;
+            }
+            if (phase == PH_SEEK1 || phase == PH_SEEK2) {
+                int at = -1, mi = 1;
+                if (phase == PH_SEEK1) {
+                    if (x < len) {
+                        if (q[x] < 4) at = x;
+                        else { ++x; continue; }
+                    } else { old_n = sn; k = 0; phase = PH_SEEK2; continue; }
+                    pass = 1;
+                } else {
+                    if (k < old_n) {
+                        const Intv p = out[k];
+                        const int st = (int)(p.info >> 32), en = (int)(uint32_t)p.info;
+                        if (en - st < split_len || p.x[2] > split_width) { ++k; continue; }
+                        at = (st + en) >> 1; mi = (int)p.x[2] + 1;
+                    } else { x = 0; phase = max_mem_intv > 0 ? PH_SEEKS : PH_FIN; continue; }
+                    pass = 2;
+                }
+                // bwt_smem1a entry
+                sx = at; n1 = 0; minI = (X)(mi < 1 ? 1 : mi);
+                const int c0 = q[at];
+                if (c0 > 3) {
+                    if (pass == 1) { x = at + 1; } else { ++k; }
+                    continue;
+                }
+                ik0 = fm.L2(c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0); ik1 = fm.L2(3 - c0) + 1;
+                ikend = at + 1; nl = 0; i = at + 1;
+                phase = PH_FWD;
+                continue;
+            }
+            if (phase == PH_SEEKS) {
+                if (x < len) {
+                    const int c0 = q[x];
+                    if (c0 > 3) { ++x; continue; }
+                    sx = x; i = x + 1;
+                    ik0 = fm.L2(c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0); ik1 = fm.L2(3 - c0) + 1;
+                    phase = PH_STF;
+                } else phase = PH_FIN;
+                continue;
+            }
+            if (phase == PH_FIN) {
+                if (ovf) {
+                    status[li] |= ST_OVERFLOW;
+                    n_intv[li] = 0;
+                } else {
+                    for (int a = 1; a < sn; ++a) {   // equal keys are identical intervals: any correct sort is exact
+                        const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
+                        int b = a;
+                        for (; b > 0; --b) {
+                            const uint64_t pi = out[b - 1].info;
+                            if (!(ti < pi)) break;
+                            out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
+                            out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
+                        }
+                        out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
+                    }
+                    n_intv[li] = sn;
+                }
+                phase = PH_NEXT;
+                continue;
+            }
+            // PH_NEXT
+            li += stride;
+            if (li >= n) { phase = PH_EXIT; continue; }
+            q = codes + offs[li];
+            len = (int)(offs[li + 1] - offs[li]);
+            out = intv_out + (size_t)li * cp.intv;
+            sn = 0; ovf = false; x = 0; qp_pos = -1;
+            phase = PH_SEEK1;
+        }
+        if (!__any(want)) break;
+        if (!want) continue;
+        if (pp >= 0 && pp != qp_pos) { qp_val = q[pp]; qp_pos = pp; }
+        extend1(fm, ea, eo, ex2, ec, r_new, r_oth, r_2, nblk);
+        // fast path: consume the result and issue the next request for the common steps; anything
+        // else leaves the result to the machine above (same state updates either way)
+        want = false;
+        if (phase == PH_FWD || phase == PH_STF) {
+            const int nxt = i + 1;
+            const int cur = nxt < len ? getq(nxt) : 4;
+            const bool fwd = phase == PH_FWD;
+            const bool changed = r_2 != ik2;
+            const bool stop = fwd ? (changed && r_2 < minI) : (r_2 < (X)max_mem_intv && i - sx >= min_seed_len);
+            if (!stop && cur < 4 && !(fwd && changed && nl >= lcap)) {
+                if (fwd && changed) { Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl; }
+                ikend = nxt; ik0 = r_oth; ik1 = r_new; ik2 = r_2; i = nxt;
+                ea = ik1; eo = ik0; ex2 = ik2; ec = 3 - cur; want = true;
+                pp = nxt + 1 < len ? nxt + 1 : -1;
+            } else have_res = true;
+        } else {   // PH_BWD: apply, then the next entry (or the next position when the level is done)
+            if (r_2 < minI) {
+                if (nc == 0 && (n1 == 0 || bi + 1 < last_start)) {
+                    ++n1; last_start = bi + 1;
+                    if (ee - (bi + 1) >= min_seed_len) {
+                        if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
+                        Intv m;
+                        m.x[0] = e0; m.x[1] = 0; m.x[2] = e2;
+                        m.info = (uint64_t)(uint32_t)(bi + 1) << 32 | (uint32_t)ee;
+                        out[sn++] = m;
+                    }
+                }
+            } else if (nc == 0 || r_2 != last_x2) {
+                const int p = (top - nc) * T;
+                Lx0[p] = r_new; Lx2[p] = r_2; Lend[p] = (uint16_t)ee;
+                ++nc; last_x2 = r_2;
+            }
+            ++j;
+            if (j == nl && nc > 0) {
+                nl = nc; --bi;
+                cb = bi < 0 ? -1 : getq(bi);
+                cb = cb < 4 ? cb : -1;
+                j = 0; nc = 0; last_x2 = 0;
+            }
+            if (j < nl && cb >= 0) {
+                const int p = (top - j) * T;
+                e0 = Lx0[p]; e2 = Lx2[p]; ee = Lend[p];
+                ea = e0; eo = 0; ex2 = e2; ec = cb; want = true; pp = bi - 1;
+            }
+        }
+    }
+    wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
+}
+
+hipError_t launch_smem_flat(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                            const int64_t *offs, int n, Intv *intv, int32_t *n_intv, uint32_t *status, Counters *ctr,
+                            int lcap, int max_blocks)
+{
+    const int T = 256;
+    int grid = (n + T - 1) / T;
+    if (grid == 0) return hipSuccess;
+    auto clamp = [&](const void *fn, size_t sh) {
+        // persistent lanes: one resident wave of blocks (or max_blocks when given)
+        int dev = 0, cus = 0, per = 0;
+        if (max_blocks <= 0 && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, T, sh) == hipSuccess && per > 0)
+            max_blocks = cus * per;
+        if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+    };
+    if (ix.seq_len < 0xFFFFFFFFull) {
+        size_t sh = lds_bytes<uint32_t>(T, lcap);
+        clamp(reinterpret_cast<const void *>(k_smem_flat<uint32_t>), sh);
+        hipLaunchKernelGGL(k_smem_flat<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
+                           status, ctr, lcap);
+    } else {
+        size_t sh = lds_bytes<uint64_t>(T, lcap);
+        clamp(reinterpret_cast<const void *>(k_smem_flat<uint64_t>), sh);
+        hipLaunchKernelGGL(k_smem_flat<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
                            status, ctr, lcap);
     }
     return hipGetLastError();
