@@ -47,6 +47,7 @@ hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Cap
                            Intv *, int32_t *, uint32_t *, Counters *, int);
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
+hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
 }  // namespace bsq
 
 using namespace bsq;
@@ -107,11 +108,12 @@ struct DeviceIndex {
     uint8_t *pac = nullptr;
     int64_t *ann_off = nullptr, *ann_id = nullptr;
     int32_t *ann_len = nullptr;
+    uint32_t *kmer = nullptr;
     DIndex view{};
     ~DeviceIndex()
     {
         if (device >= 0) hipSetDevice(device);
-        hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len);
+        hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len); hipFree(kmer);
     }
 };
 }  // namespace bsq
@@ -229,6 +231,23 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
     v.primary = h.primary;
     v.seq_len = h.seq_len;
     v.l_pac = h.l_pac;
+    v.kmer = nullptr;
+    v.kmer_k = 0;
+    // k-mer interval table (u32 rows): depth ~log4(rows), at most 11 (89 MB, stays in the Infinity
+    // Cache beside the occ array at 100 Mbp); BSQ_KMER_K overrides, 0 disables
+    if (h.seq_len > 0 && h.seq_len < 0xFFFFFFFFull) {
+        int K = 0;
+        while (K < 11 && (1ull << (2 * (K + 1))) <= h.seq_len) ++K;
+        if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
+        if (K > 0) {
+            const size_t entries = (((size_t)1 << (2 * (K + 1))) - 4) / 3;
+            HIPCHK(hipMalloc(&d->kmer, entries * 16));
+            v.kmer = d->kmer;
+            HIPCHK(launch_kmer_build(nullptr, v, d->kmer, K));
+            HIPCHK(hipDeviceSynchronize());
+            v.kmer_k = K;
+        }
+    }
     return BSQ_OK;
 }
 
@@ -701,7 +720,8 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         }
         Counters c[STG_N];
         HIPCHK(hipMemcpy(c, b->ctr, sizeof c, hipMemcpyDeviceToHost));
-        b->stage_bytes[STG_SMEM] = 64.0 * c[STG_SMEM].occ_blocks + (double)b->h_offs[n] / 4.0 * 1.0;
+        b->stage_bytes[STG_SMEM] =
+            64.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
         b->stage_bytes[STG_CHAIN] = 8.0 * c[STG_CHAIN].sa_values;
         b->stage_bytes[STG_EXTEND] = (double)c[STG_EXTEND].ref_bases;
         b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;

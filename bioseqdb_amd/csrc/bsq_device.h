@@ -24,10 +24,14 @@ struct DIndex {
     const int64_t *ann_off;   // bntann1_t.offset per reference row
     const int32_t *ann_len;   // bntann1_t.len
     int32_t n_anns;
-    int32_t pad;
+    int32_t kmer_k;           // k-mer interval table depth (0 = none)
     uint64_t L2[5];
     uint64_t primary, seq_len;
     int64_t l_pac;
+    // k-mer interval table: for every string S over ACGT with 1 <= |S| <= kmer_k, the bidirectional
+    // interval (x[0], x[1], x[2], 0) that bwt_extend chains produce for S (u32 rows only), at entry
+    // (4^|S| - 4)/3 + code(S), code = base-4 value of S with the first base most significant
+    const uint32_t *kmer;
 };
 
 // mem_opt_t fields the path reads (mem_opt_init defaults + bioseqdb overrides).
@@ -77,7 +81,8 @@ struct Counters {
     unsigned long long ref_bases;    // reference bases fetched for extension / CIGAR
     unsigned long long dp_cells;     // DP cells evaluated (secondary figure)
     unsigned long long overflow;     // reads flagged for the retry pass
-    unsigned long long pad[3];
+    unsigned long long kmer_hits;    // 16-B k-mer interval table reads (in place of a bwt_extend)
+    unsigned long long pad[2];
 };
 
 }  // namespace bsq

@@ -23,6 +23,8 @@ namespace bsq {
 template <typename X>
 struct FM {
     const OccBlock *occ;
+    const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
+    int K;
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
     DEV X L2(int c) const { return c == 0 ? l2_0 : c == 1 ? l2_1 : c == 2 ? l2_2 : c == 3 ? l2_3 : l2_4; }
 };
@@ -83,7 +85,7 @@ DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, u
 // Two independent backward extensions by the same base (entries of one bwt_smem1 backward level);
 // all four occ blocks are in flight together.  Backward extensions only need (x[0], x[2]).
 template <typename X>
-DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool hb, int c, X &ra0, X &ra2, X &rb0, X &rb2,
+DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, int c, X &ra0, X &ra2, X &rb0, X &rb2,
                    uint64_t &nblk)
 {
     const X ka = a0 - 1, la = a0 - 1 + a2;
@@ -96,10 +98,14 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool hb, int c, X &r
     const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ + (kbn ? 0 : (kkb >> 7)));
     const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ + (llb >> 7));
     uint4 w0[4], w1[4], w2[4], w3[4];
-    w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
-    w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
-    w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
-    w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
+    if (da) {
+        w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
+        w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
+    }
+    if (hb) {
+        w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
+        w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
+    }
     X kc, kg, lc, lg;
     occ_c(w0, kka, kan, c, kc, kg);
     occ_c(w1, lla, false, c, lc, lg);
@@ -109,9 +115,12 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool hb, int c, X &r
     occ_c(w3, llb, false, c, lc, lg);
     rb0 = fm.L2(c) + 1 + kc;
     rb2 = lc - kc;
-    nblk += (kan || (kka >> 7) == (lla >> 7)) ? 1 : 2;
+    if (da) nblk += (kan || (kka >> 7) == (lla >> 7)) ? 1 : 2;
     if (hb) nblk += (kbn || (kkb >> 7) == (llb >> 7)) ? 1 : 2;
 }
+
+// first entry of the k-mer table level for strings of length L: (4^L - 4) / 3
+DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
 
 // LDS list of (x0, x2, end) entries for one lane: entry e at base[e * stride]
 template <typename X>
@@ -129,7 +138,7 @@ struct OutSlot {   // the read's output intervals (global), mem grows from the f
 
 template <typename X>
 DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_intv, LList<X> &L, OutSlot &S,
-                  bool &ovf, uint64_t &nblk)
+                  bool &ovf, uint64_t &nblk, uint64_t &nkm)
 {
     S.n1 = 0;
     if (q[x] > 3) return x + 1;
@@ -139,13 +148,19 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     int ikend = x + 1;
     int n = 0, i;
     int qi = x + 1 < len ? q[x + 1] : 0;
+    uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
     for (i = x + 1; i < len; ++i) {
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;   // prefetch the next base
         if (cur < 4) {
             const int c = 3 - cur;
             X n1, n0, n2;
-            extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
+            fcode = fcode << 2 | (uint32_t)cur;
+            if (i - x + 1 <= fm.K) {
+                const uint4 e = fm.kt[koff(i - x + 1) + fcode];
+                n0 = (X)e.x; n1 = (X)e.y; n2 = (X)e.z;
+                ++nkm;
+            } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 != ik2) {
                 if (n >= L.cap) { ovf = true; return len; }
                 L.set(n++, ik0, ik2, ikend);
@@ -171,8 +186,12 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     }
     const int ret = L.end[0];
     int last_start = 0x7fffffff;
+    const int K = fm.K;
+    uint32_t wcode = 0;   // q[i .. i+K) packed, first base most significant (positions past the read: 0)
+    for (int t = 0; t < K; ++t) wcode = wcode << 2 | (x + t < len ? (uint32_t)(q[x + t] & 3) : 0u);
     for (i = x - 1; i >= -1; --i) {
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+        if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
         int nc = 0;
         X last_x2 = 0;
         for (int j = 0; j < n; j += 2) {
@@ -185,7 +204,18 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
             const X pb0 = L.x0[jb * L.stride], pb2 = L.x2[jb * L.stride];
             const int pbe = L.end[jb * L.stride];
             X oa0 = 0, oa2 = 0, ob0 = 0, ob2 = 0;
-            if (c >= 0) ext_back2(fm, pa0, pa2, pb0, pb2, hb, c, oa0, oa2, ob0, ob2, nblk);
+            if (c >= 0) {
+                // strings q[i .. end) of at most K bases come from the k-mer table
+                const int La = pae - i, Lb = pbe - i;
+                const bool ta = La <= K, tb = hb && Lb <= K;
+                uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
+                if (ta) ea = fm.kt[koff(La) + (wcode >> (2 * (K - La)))];
+                if (tb) eb = fm.kt[koff(Lb) + (wcode >> (2 * (K - Lb)))];
+                nkm += (uint64_t)ta + (uint64_t)tb;
+                if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
+                if (ta) { oa0 = (X)ea.x; oa2 = (X)ea.z; }
+                if (tb) { ob0 = (X)eb.x; ob2 = (X)eb.z; }
+            }
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && !hb) break;
                 const X p0 = h ? pb0 : pa0, p2 = h ? pb2 : pa2, o0 = h ? ob0 : oa0, o2 = h ? ob2 : oa2;
@@ -214,20 +244,26 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
 
 template <typename X>
 DEV int seed_strategy1_x(const FM<X> &fm, int len, const uint8_t *q, int x, int min_len, int max_intv, Intv &mem,
-                         uint64_t &nblk)
+                         uint64_t &nblk, uint64_t &nkm)
 {
     mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
     if (q[x] > 3) return x + 1;
     const int c0 = q[x];
     X ik0 = fm.L2(c0) + 1, ik2 = fm.L2(c0 + 1) - fm.L2(c0), ik1 = fm.L2(3 - c0) + 1;
     int qi = x + 1 < len ? q[x + 1] : 0;
+    uint32_t fcode = (uint32_t)c0;
     for (int i = x + 1; i < len; ++i) {
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;
         if (cur < 4) {
             const int c = 3 - cur;
             X n1, n0, n2;
-            extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
+            fcode = fcode << 2 | (uint32_t)cur;
+            if (i - x + 1 <= fm.K) {
+                const uint4 e = fm.kt[koff(i - x + 1) + fcode];
+                n0 = (X)e.x; n1 = (X)e.y; n2 = (X)e.z;
+                ++nkm;
+            } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 < (X)max_intv && i - x >= min_len) {
                 mem.x[0] = n0; mem.x[1] = n1; mem.x[2] = n2;
                 mem.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
@@ -262,7 +298,9 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     fm.occ = ix.occ;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
-    uint64_t nblk = 0;
+    fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
+    fm.K = sizeof(X) == 4 ? ix.kmer_k : 0;
+    uint64_t nblk = 0, nkm = 0;
     const int li = blockIdx.x * T + t;
     if (li < n) {
         const uint8_t *q = codes + offs[li];
@@ -284,7 +322,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
         int x = 0;
         while (x < len && !ovf) {
             if (q[x] < 4) {
-                x = smem1_lds(fm, len, q, x, 1, L, S, ovf, nblk);
+                x = smem1_lds(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
                 if (!ovf) take_mem1(false);
             } else ++x;
         }
@@ -293,7 +331,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             const Intv p = S.a[k];
             const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
             if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) continue;
-            smem1_lds(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk);
+            smem1_lds(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
             if (!ovf) take_mem1(true);
         }
         if (o.max_mem_intv > 0) {
@@ -301,7 +339,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             while (x < len && !ovf) {
                 if (q[x] < 4) {
                     Intv m;
-                    x = seed_strategy1_x(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk);
+                    x = seed_strategy1_x(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm);
                     if (m.x[2] > 0) {
                         if (S.n >= S.cap) { ovf = true; break; }
                         Intv &d = S.a[S.n++];
@@ -330,6 +368,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
         }
     }
     wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
+    wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
 }
 
 // LDS bytes per thread for `lcap` list entries
@@ -383,6 +422,8 @@ __global__ void __launch_bounds__(256) k_smem_flat(DIndex ix, DOpts o, Caps cp, 
     fm.occ = ix.occ;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
+    fm.kt = nullptr;
+    fm.K = 0;
     const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
     const int min_seed_len = o.min_seed_len;
     const uint64_t split_width = (uint64_t)o.split_width;
@@ -649,6 +690,62 @@ hipError_t launch_smem_flat(hipStream_t st, const DIndex &ix, const DOpts &o, co
         clamp(reinterpret_cast<const void *>(k_smem_flat<uint64_t>), sh);
         hipLaunchKernelGGL(k_smem_flat<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
                            status, ctr, lcap);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// k-mer interval table build (index upload): level 1 from L2, level L+1 from level L by one full
+// backward bwt_extend per parent (prepending base c to S gives code c * 4^L + code(S)).  The
+// bidirectional interval of a string does not depend on the extension path that reached it, so a
+// table entry equals what the kernels' forward or backward extend chains compute for that string
+// (only non-empty intervals are ever consumed; empty ones are only compared against x[2] bounds).
+__global__ void k_kmer_level(DIndex ix, uint4 *tab, int L)
+{
+    const uint64_t n = 1ull << (2 * L);
+    const uint64_t P = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L == 0) {
+        if (P < 4) {
+            const int c = (int)P;
+            tab[P] = make_uint4((uint32_t)ix.L2[c] + 1, (uint32_t)ix.L2[3 - c] + 1,
+                                (uint32_t)(ix.L2[c + 1] - ix.L2[c]), 0u);
+        }
+        return;
+    }
+    if (P >= n) return;
+    FM<uint32_t> fm;
+    fm.occ = ix.occ;
+    fm.kt = nullptr;
+    fm.K = 0;
+    fm.l2_0 = (uint32_t)ix.L2[0]; fm.l2_1 = (uint32_t)ix.L2[1]; fm.l2_2 = (uint32_t)ix.L2[2];
+    fm.l2_3 = (uint32_t)ix.L2[3]; fm.l2_4 = (uint32_t)ix.L2[4];
+    fm.primary = (uint32_t)ix.primary;
+    const uint4 e = tab[koff(L) + P];
+    const uint32_t x0 = e.x, x1 = e.y, x2 = e.z;
+    uint32_t o0[4], o2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t na, no, nx2;
+        uint64_t nb = 0;
+        extend1(fm, x0, 0u, x2, c, na, no, nx2, nb);
+        o0[c] = na; o2[c] = nx2;
+    }
+    const uint32_t x1_3 = x1 + (uint32_t)(x0 <= fm.primary && x0 + x2 - 1 >= fm.primary);
+    const uint32_t x1_2 = x1_3 + o2[3], x1_1 = x1_2 + o2[2], x1_0 = x1_1 + o2[1];
+    uint4 *dst = tab + koff(L + 1) + P;
+    dst[0 * n] = make_uint4(o0[0], x1_0, o2[0], 0u);
+    dst[1 * n] = make_uint4(o0[1], x1_1, o2[1], 0u);
+    dst[2 * n] = make_uint4(o0[2], x1_2, o2[2], 0u);
+    dst[3 * n] = make_uint4(o0[3], x1_3, o2[3], 0u);
+}
+
+hipError_t launch_kmer_build(hipStream_t st, const DIndex &ix, uint32_t *tab, int K)
+{
+    uint4 *t = reinterpret_cast<uint4 *>(tab);
+    hipLaunchKernelGGL(k_kmer_level, dim3(1), dim3(64), 0, st, ix, t, 0);
+    for (int L = 1; L < K; ++L) {
+        const uint64_t n = 1ull << (2 * L);
+        hipLaunchKernelGGL(k_kmer_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, t, L);
     }
     return hipGetLastError();
 }
