@@ -30,6 +30,20 @@ from bioseqdb_amd import _native as N  # noqa: E402
 
 METRIC = "aligned reads/sec (150 bp vs 100 Mbp ref) at 1/2/4/8 MI355X; bit-exact vs libbwa"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# stage -> the main-pass kernel its HIP events bracket (libbsq run_stages)
+STAGE_KERNEL = {"smem": "k_smem_lds", "chain": "k_chain", "extend": "k_extend", "reg2aln": "k_reg2aln_w"}
+# per-launch HBM traffic from the committed PMC passes (tools/profile_round.sh + tools/traffic_from_pmc.py,
+# FETCH_SIZE corrected by the calib_fetch.hip gather calibration); PMC cannot be collected in-process
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def traffic_for(stage: str, reads: int):
+    try:
+        t = json.load(open(TRAFFIC_JSON))
+        k = t["kernels"][stage]
+        return k["traffic_bytes"] * reads / t["reads_per_launch"], t["round"]
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def log(*a):
@@ -194,9 +208,19 @@ def main() -> int:
             "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
         },
         "roofline": {
-            "bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_for(dom, args.reads)[0],
+            "traffic_source": f"profiles/traffic.json ({traffic_for(dom, args.reads)[1]} PMC FETCH_SIZE+WRITE_SIZE per launch)",
             "algorithmic_bytes_per_launch": float(stage_bytes[di]), "launch_ms": round(float(stage_ms[di]), 3),
+        },
+        "kernels": {
+            STAGE_KERNEL[nm]: {
+                "ms": round(float(stage_ms[i]), 3), "algorithmic_bytes": float(stage_bytes[i]),
+                "achieved_gbs": round(stage_bytes[i] / (stage_ms[i] * 1e-3) / 1e9, 2) if stage_ms[i] > 0 else 0.0,
+                "traffic_bytes": traffic_for(nm, args.reads)[0],
+                "traffic_gbs": (round(traffic_for(nm, args.reads)[0] / (stage_ms[i] * 1e-3) / 1e9, 2)
+                                if traffic_for(nm, args.reads)[0] and stage_ms[i] > 0 else None),
+            } for i, nm in enumerate(names[:4])
         },
         "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
         "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the alignment kernels from rocprofv3 PMC passes (tools/profile_round.sh).
+
+FETCH_SIZE / WRITE_SIZE are summed per dispatch (KB -> bytes).  Correction (MI355X_MICROARCH.md, HBM
+section: calibrate non-streaming widths on a known byte count): tools/calib_fetch.hip measured on the
+same box gives FETCH_SIZE = 1.00 x bytes for random 64-B block gathers (the occ rank query, the
+dominant access of every kernel here) and 0.5 x for 16-B/lane coalesced streaming; the kernels'
+accesses are gathers, so the factor applied is the gather64 ratio.  Writes are taken as reported.
+Usage: traffic_from_pmc.py <profile dir> <out json> <round tag>
+"""
+import csv, glob, json, os, sys
+
+KERNELS = {"smem": "k_smem_lds<unsigned int>", "chain": "bsq::k_chain", "extend": "k_extend<true>",
+           "reg2aln": "bsq::k_reg2aln_w"}
+
+
+def per_dispatch(d, counter):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024.0)
+    return out
+
+
+def main(root, dst, tag):
+    cal = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0)
+                 for f in glob.glob(os.path.join(root, "calib", "**", "*counter_collection.csv"), recursive=True)
+                 for r in csv.DictReader(open(f)))
+    cal = [c for c in cal if c[1].startswith("k_")]
+    gib = float(1 << 30)
+    names = ["stream_4G", "gather64_4G", "gather16_4G", "stream_96M_warm", "gather64_96M", "gather16_96M"]
+    calib = {names[i]: round(c[2] / (gib if i != 3 else 96 * (1 << 20)), 4) for i, c in enumerate(cal[:6])}
+    corr = calib.get("gather64_4G", 1.0)
+    fetch, write = per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE"), per_dispatch(os.path.join(root, "write"), "WRITE_SIZE")
+    res = {"round": tag, "reads_per_launch": 1000000, "fetch_correction": 1.0 / corr,
+           "calibration_fetch_size_over_bytes": calib, "kernels": {}}
+    for stage, pat in KERNELS.items():
+        fk = [k for k in fetch if pat in k]
+        wk = [k for k in write if pat in k]
+        if not fk or not wk:
+            continue
+        fb = sum(fetch[fk[0]]) / len(fetch[fk[0]])
+        wb = sum(write[wk[0]]) / len(write[wk[0]])
+        res["kernels"][stage] = {"kernel": fk[0].split("(")[0], "fetch_bytes": fb / corr, "write_bytes": wb,
+                                 "traffic_bytes": fb / corr + wb}
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
