@@ -152,6 +152,7 @@ def main() -> int:
         step()
     stage_ms = np.zeros(6)
     stage_bytes = np.zeros(6)
+    stage_work = np.zeros(6)
     if dist is not None:
         import torch
         dist.barrier()
@@ -163,6 +164,9 @@ def main() -> int:
         L.bsq_batch_stage_ms(batch, ms, 6)
         by = (ctypes.c_double * 6)()
         L.bsq_batch_stage_bytes(batch, by, 6)
+        wk = (ctypes.c_double * 6)()
+        L.bsq_batch_stage_work(batch, wk, 6)
+        stage_work += np.array(list(wk))
         stage_ms += np.array(list(ms))
         stage_bytes += np.array(list(by))
     if dist is not None:
@@ -177,6 +181,7 @@ def main() -> int:
         elapsed = float(t.item())
     stage_ms /= max(args.steps, 1)
     stage_bytes /= max(args.steps, 1)
+    stage_work /= max(args.steps, 1)
     H = L.bsq_batch_hits(batch).contents
     n_hits = int(H.n_hits)
     retried = int(L.bsq_batch_retried(batch))
@@ -218,6 +223,7 @@ def main() -> int:
                 "ms": round(float(stage_ms[i]), 3), "algorithmic_bytes": float(stage_bytes[i]),
                 "achieved_gbs": round(stage_bytes[i] / (stage_ms[i] * 1e-3) / 1e9, 2) if stage_ms[i] > 0 else 0.0,
                 "traffic_bytes": traffic_for(nm, args.reads)[0],
+                "work": float(stage_work[i]),
                 "traffic_gbs": (round(traffic_for(nm, args.reads)[0] / (stage_ms[i] * 1e-3) / 1e9, 2)
                                 if traffic_for(nm, args.reads)[0] and stage_ms[i] > 0 else None),
             } for i, nm in enumerate(names[:4])

@@ -89,6 +89,7 @@ SIGNATURES = {
     "bsq_batch_stage_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "bsq_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "bsq_batch_stage_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    "bsq_batch_stage_work": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "bsq_batch_retried": (ctypes.c_int64, [_P]),
 }
 

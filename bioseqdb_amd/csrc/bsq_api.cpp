@@ -393,6 +393,7 @@ struct bsq_batch {
     hipEvent_t ev[STG_N + 1]{};
     float stage_ms[STG_N]{};
     double stage_bytes[STG_N]{};
+    double stage_work[STG_N]{};
     int64_t retried = 0;
 };
 
@@ -727,8 +728,10 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;
         b->stage_bytes[STG_PACK] = (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
+        for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
+        b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks;
     } else {
-        for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; }
+        for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
     b->view.n_reads = n;
     b->view.n_hits = (int64_t)b->res_hits.size();
@@ -752,6 +755,13 @@ extern "C" int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max)
 {
     if (!b) return 0;
     for (int s = 0; s < STG_N && s < max; ++s) bytes[s] = b->stage_bytes[s];
+    return STG_N;
+}
+
+extern "C" int bsq_batch_stage_work(const bsq_batch *b, double *work, int max)
+{
+    if (!b) return 0;
+    for (int s = 0; s < STG_N && s < max; ++s) work[s] = b->stage_work[s];
     return STG_N;
 }
 

@@ -158,28 +158,42 @@ DEV int wave_shl1(int v, int last) { return __builtin_amdgcn_update_dpp(last, v,
 //   s == 1: Hd' = h of lane l,                                        E' = e_new of lane l+1
 // (-inf for the new column's E) -- exactly the eh[] values the serial kernel would read.
 template <bool ZL>
-DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_dir, TStream ts, int tlen, int o_del,
-                        int e_del, int o_ins, int e_ins, int w, int n_col, int z_off, uint8_t *zg, uint64_t &cells)
+DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_dir, const DIndex &ix, int64_t t_start,
+                        int t_dir, int tlen, int o_del, int e_del, int o_ins, int e_ins, int w, int n_col, int z_off,
+                        uint8_t *zg, uint64_t &cells)
 {
     const int l = lane_id();
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    // both sequences in registers, so the row loop has no memory wait: the target 2 bits per base, 16
+    // per lane (row i's base = a scalar readlane); the query 4 bits per base, 8 per lane, plus qv =
+    // q[beg + l], the band's columns, shifted along with the band
+    uint32_t tw = 0;
+    for (int k = 0; k < 16; ++k) {
+        const int i = l * 16 + k;
+        if (i < tlen) tw |= (uint32_t)ref_at(ix, t_start + (int64_t)t_dir * i) << (2 * k);
+    }
+    uint32_t qpk = 0;
+    for (int k = 0; k < 8; ++k) {
+        const int j = l * 8 + k;
+        const uint32_t v = j < qlen ? (uint32_t)g_lds_dp[q_off + q_start + q_dir * j] : 4u;
+        qpk |= v << (4 * k);
+    }
+    int qv = l < qlen ? g_lds_dp[q_off + q_start + q_dir * l] : 4;
     int Hd = l == 0 ? 0 : (l <= w ? -(o_ins + e_ins * l) : MINUS_INF_W);
     int E = MINUS_INF_W;
-    int beg = 0, last_end = 0, h_last = 0;
+    int beg = 0, last_end = 0, width = 0, h = 0;
     for (int i = 0; i < tlen; ++i) {
-        const int tb = ts.next();
+        const int tb = (int)((uint32_t)__builtin_amdgcn_readlane((int)tw, i >> 4) >> (2 * (i & 15))) & 3;
         const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
-        const int width = end - beg;
+        width = end - beg;
         const bool act = l < width;
-        const int j = beg + l;
-        const int qv = act ? g_lds_dp[q_off + q_start + q_dir * j] : 0;
         const int m = Hd + sc(tb, qv);
         const int tf = m - oe_ins;
         const int ex = wave_excl_max(act ? tf + l * e_ins : NEG_SCAN);
         int f = MINUS_INF_W - l * e_ins;
         if (l > 0) { const int fs = ex - (l - 1) * e_ins; f = f > fs ? f : fs; }
         int d = m >= E ? 0 : 1;
-        int h = m >= E ? m : E;
+        h = m >= E ? m : E;
         d = h >= f ? d : 2;
         h = h >= f ? h : f;
         const int te = m - oe_del, e2 = E - e_del;
@@ -192,7 +206,6 @@ DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_
             else zg[i * n_col + l] = (uint8_t)d;
         }
         cells += (uint64_t)width;
-        h_last = __builtin_amdgcn_readlane(h, width - 1);
         last_end = end;
         const int beg_next = i + 1 > w ? i + 1 - w : 0;
         if (beg_next == beg) {
@@ -202,10 +215,13 @@ DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_
             Hd = h;
             const int es = wave_shl1(enew, MINUS_INF_W);
             E = l + 1 < width ? es : MINUS_INF_W;
+            const int jn = beg_next + 63;   // column entering lane 63
+            const int qn = jn < qlen ? (int)((uint32_t)__builtin_amdgcn_readlane((int)qpk, jn >> 3) >> (4 * (jn & 7))) & 15 : 4;
+            qv = wave_shl1(qv, qn);
         }
         beg = beg_next;
     }
-    if (last_end == qlen) return h_last;
+    if (tlen > 0 && last_end == qlen) return __builtin_amdgcn_readlane(h, width - 1);
     return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
 }
 
@@ -275,16 +291,15 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
         const int min_w = dl + 3;
         w = w > min_w ? w : min_w;
         const int n_col = l_query < 2 * w + 1 ? l_query : 2 * w + 1;
-        if (n_col <= 64 && rlen < (int64_t)l_query + w && !(o.exp_flags & 4)) {
-            // register-resident rows; traceback matrix in LDS (z_off >= 0) or the global slab
+        if (n_col <= 64 && rlen < (int64_t)l_query + w && rlen <= 1024 && l_query <= 512 && !(o.exp_flags & 4)) {
+            // register-resident rows and sequences; traceback matrix in LDS (z_off >= 0) or the global slab
             if ((int64_t)n_col * rlen > zcap) { ovf = true; return 0; }
-            TStream ts;
-            ts.init(ix, ta.start, ta.dir);
             const bool zl = z_off >= 0;
-            *score = zl ? ksw_global2_reg<true>(score_of(o), l_query, q_off, qa.start, qa.dir, ts, (int)rlen, o.o_del,
-                                                o.e_del, o.o_ins, o.e_ins, w, n_col, z_off, nullptr, cells)
-                        : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ts, (int)rlen, o.o_del,
-                                                 o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
+            *score = zl ? ksw_global2_reg<true>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
+                                                (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, z_off,
+                                                nullptr, cells)
+                        : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
+                                                 (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
             if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
             if (zl) traceback_w<true>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
             else traceback_w<false>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
@@ -297,12 +312,16 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
 }
 
 // mem_reg2aln per region, one wave per read.  LDS per wave: eh (max_len+2 int2) + z (zcap bytes).
-__global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
-                                                   const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs,
-                                                   Hit *hits, uint32_t *cigars, int32_t *n_cig_read, uint32_t *status,
-                                                   Counters *ctr, int zcap, uint8_t *zslab, int64_t zslab_bytes)
+__global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, const uint8_t *__restrict__ codes,
+                                                   const int64_t *__restrict__ offs, int n,
+                                                   const Reg *__restrict__ regs, const int32_t *__restrict__ n_regs,
+                                                   Hit *__restrict__ hits, uint32_t *__restrict__ cigars,
+                                                   int32_t *__restrict__ n_cig_read, uint32_t *__restrict__ status,
+                                                   Counters *ctr, int zcap, uint8_t *__restrict__ zslab,
+                                                   int64_t zslab_bytes)
 {
-    const int wave = threadIdx.x >> 6;
+    // the control below is wave-uniform: make that visible so it lives in SGPRs / scalar loads
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
     const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
     const size_t per_wave = eh_bytes + (size_t)zcap + q_bytes;

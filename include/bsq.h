@@ -146,6 +146,9 @@ const char *bsq_stage_name(int stage);
 /* Algorithmic bytes of the last run (SURVEY.md §8(d) counting), per stage: occ-block fetches x64,
  * SA values x8, reference windows ceil(bases/4), reads and hit records.  Returns stages written. */
 int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max);
+/* Work counters of the last run, per stage: DP cells evaluated (extend, reg2aln) and, for the
+ * seeding stage, bwt_extend-equivalent steps (occ-block pairs + k-mer table reads).  Diagnostics. */
+int bsq_batch_stage_work(const bsq_batch *b, double *work, int max);
 /* Number of reads of the last run that needed the large-capacity retry pass. */
 int64_t bsq_batch_retried(const bsq_batch *b);
 
