@@ -40,9 +40,9 @@ hipError_t launch_counts(hipStream_t, int, const SlotView &, const SlotView &, c
 hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const int64_t *,
                        const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *);
 hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
-hipError_t launch_reg2aln_w(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
-                            int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *, uint32_t *, Counters *, int,
-                            uint8_t *, int64_t, int);
+hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *,
+                                const int64_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *,
+                                uint32_t *, Counters *, int, uint8_t *, int64_t, int, int32_t *, int32_t *, int32_t *);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int);
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
@@ -291,12 +291,13 @@ struct Workspace {
     uint8_t *zslab = nullptr; // per-wave traceback spill slabs of the wave reg2aln kernel
     int64_t zslab_bytes = 0;
     int zslab_blocks = 0;
+    int32_t *dlist0 = nullptr, *dlist1 = nullptr, *dcount = nullptr;   // reads deferred by the group kernels
 
     void release()
     {
         hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
-        hipFree(zslab);
+        hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
         *this = Workspace{};
     }
 };
@@ -338,6 +339,9 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         w.zslab_bytes = (int64_t)(2 * cp.max_len + 8) * (int64_t)(2 * cp.max_len + 64);
         w.zslab_blocks = (int)std::min<int64_t>(((int64_t)R + 3) / 4, 3 * 256);
         HIPCHK(hipMalloc(&w.zslab, (size_t)w.zslab_blocks * 4 * (size_t)w.zslab_bytes));
+        HIPCHK(hipMalloc(&w.dlist0, R * 4));
+        HIPCHK(hipMalloc(&w.dlist1, R * 4));
+        HIPCHK(hipMalloc(&w.dcount, 16));
     }
     return BSQ_OK;
 }
@@ -550,8 +554,9 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int64_t q_bytes = ((int64_t)w.cp.max_len + 16) & ~15LL;
         const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes - q_bytes) & ~15;
         // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
-        HIPCHK(launch_reg2aln_w(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
-                                w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks));
+        HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
+                                    w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
+                                    w.dlist0, w.dlist1, w.dcount));
     } else {
         HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars,
                               w.n_cig, w.status, w.scratch, b->ctr));

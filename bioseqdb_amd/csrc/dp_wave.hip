@@ -318,7 +318,8 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
                                                    Hit *__restrict__ hits, uint32_t *__restrict__ cigars,
                                                    int32_t *__restrict__ n_cig_read, uint32_t *__restrict__ status,
                                                    Counters *ctr, int zcap, uint8_t *__restrict__ zslab,
-                                                   int64_t zslab_bytes)
+                                                   int64_t zslab_bytes, const int32_t *__restrict__ list,
+                                                   const int32_t *__restrict__ list_n)
 {
     // the control below is wave-uniform: make that visible so it lives in SGPRs / scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -332,7 +333,9 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
     const int gw = blockIdx.x * (blockDim.x >> 6) + wave, nw = gridDim.x * (blockDim.x >> 6);
     uint8_t *z_glob = zslab + (size_t)gw * (size_t)zslab_bytes;   // this wave's spill slab
     uint64_t cells = 0, bases = 0;
-    for (int li = gw; li < n; li += nw) {
+    const int n_items = list ? *list_n : n;   // reads deferred by the group kernels, or all reads
+    for (int it_ = gw; it_ < n_items; it_ += nw) {
+    const int li = list ? list[it_] : it_;
     if (status[li]) { n_cig_read[li] = 0; continue; }
     {
         const uint8_t *q = codes + offs[li];
@@ -414,7 +417,8 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
 hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                             const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
                             uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
-                            uint8_t *zslab, int64_t zslab_bytes, int max_blocks)
+                            uint8_t *zslab, int64_t zslab_bytes, int max_blocks, const int32_t *list,
+                            const int32_t *list_n)
 {
     const int waves = 4;
     int grid = (n + waves - 1) / waves;
@@ -424,8 +428,288 @@ hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, co
     const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
     const size_t sh = (size_t)waves * (eh_bytes + (size_t)zcap + q_bytes);
     hipLaunchKernelGGL(k_reg2aln_w, dim3(grid), dim3(64 * waves), sh, st, ix, o, cp, codes, offs, n, regs, n_regs, hits,
-                       cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes);
+                       cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes, list, list_n);
     return hipGetLastError();
+}
+
+// ================================================================================================
+// Group mode: 64/G reads per wave, one per G-lane group (G = 16: one DPP row; G = 32: two rows),
+// for reads whose every ksw_global2 band fits G columns -- the common case (the band is ~10k+3
+// columns for a read with k mismatches).  Control is per group (uniform within it); the DP row
+// update is the register-row recurrence of ksw_global2_reg with segment-local DPP.  A read that
+// needs a wider band (or a bigger traceback matrix than its LDS slice) is appended to `defer`
+// before it is aligned and goes to the next kernel (G = 32, then the whole-wave kernel), which
+// recomputes it from scratch, so the output is independent of the path.
+// ================================================================================================
+template <int G> DEV int grp_excl_max(int v, int gl);
+template <> DEV int grp_excl_max<16>(int v, int gl)
+{
+    DPP_STEP(v, 0x111, 0xf);
+    DPP_STEP(v, 0x112, 0xf);
+    DPP_STEP(v, 0x114, 0xf);
+    DPP_STEP(v, 0x118, 0xf);
+    return __builtin_amdgcn_update_dpp(NEG_SCAN, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+}
+template <> DEV int grp_excl_max<32>(int v, int gl)
+{
+    DPP_STEP(v, 0x111, 0xf);
+    DPP_STEP(v, 0x112, 0xf);
+    DPP_STEP(v, 0x114, 0xf);
+    DPP_STEP(v, 0x118, 0xf);
+    DPP_STEP(v, 0x142, 0xa);   // row_bcast:15 into rows 1 and 3: 32-lane segment scan
+    const int sv = __builtin_amdgcn_update_dpp(NEG_SCAN, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    return gl == 0 ? NEG_SCAN : sv;
+}
+// lane gl receives v of gl-1 (gl = 0: `first`)
+template <int G> DEV int grp_shr1(int v, int first, int gl)
+{
+    if (G == 16) return __builtin_amdgcn_update_dpp(first, v, 0x111, 0xf, 0xf, false);
+    const int sv = __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);
+    return gl == 0 ? first : sv;
+}
+// lane gl receives v of gl+1 (gl = G-1: `last`)
+template <int G> DEV int grp_shl1(int v, int last, int gl)
+{
+    if (G == 16) return __builtin_amdgcn_update_dpp(last, v, 0x101, 0xf, 0xf, false);
+    const int sv = __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
+    return gl == G - 1 ? last : sv;
+}
+template <int G> DEV int grp_sum(int v)
+{
+#pragma unroll
+    for (int off = G >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, G);
+    return v;
+}
+
+// ksw_global2 (global mode) for bands of at most G columns: rows as in ksw_global2_reg; target and
+// query bases staged in the group's LDS slice, read one row ahead.
+template <int G>
+DEV int ksw_global2_g(const Score sc, int qlen, int q_off, int q_start, int q_dir, int t_off, int tlen, int o_del,
+                      int e_del, int o_ins, int e_ins, int w, int n_col, int z_off, uint64_t &cells, int gl)
+{
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    int qv = gl < qlen ? g_lds_dp[q_off + q_start + q_dir * gl] : 4;
+    int Hd = gl == 0 ? 0 : (gl <= w ? -(o_ins + e_ins * gl) : MINUS_INF_W);
+    int E = MINUS_INF_W;
+    int beg = 0, last_end = 0, width = 0, h = 0;
+    int tb = tlen > 0 ? g_lds_dp[t_off] : 0;
+    for (int i = 0; i < tlen; ++i) {
+        const int beg_next = i + 1 > w ? i + 1 - w : 0;
+        const int tb_n = i + 1 < tlen ? g_lds_dp[t_off + i + 1] : 0;
+        const int jn = beg_next + G - 1;
+        const int qn = (beg_next != beg && jn < qlen) ? g_lds_dp[q_off + q_start + q_dir * jn] : 4;
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        width = end - beg;
+        const bool act = gl < width;
+        const int m = Hd + sc(tb, qv);
+        const int tf = m - oe_ins;
+        const int ex = grp_excl_max<G>(act ? tf + gl * e_ins : NEG_SCAN, gl);
+        int f = MINUS_INF_W - gl * e_ins;
+        if (gl > 0) { const int fs = ex - (gl - 1) * e_ins; f = f > fs ? f : fs; }
+        int d = m >= E ? 0 : 1;
+        h = m >= E ? m : E;
+        d = h >= f ? d : 2;
+        h = h >= f ? h : f;
+        const int te = m - oe_del, e2 = E - e_del;
+        d |= e2 > te ? 1 << 2 : 0;
+        const int enew = e2 > te ? e2 : te;
+        const int f2 = f - e_ins;
+        d |= f2 > tf ? 2 << 4 : 0;
+        if (act) g_lds_dp[z_off + i * n_col + gl] = (uint8_t)d;
+        cells += (uint64_t)width;
+        last_end = end;
+        if (beg_next == beg) {
+            Hd = grp_shr1<G>(h, -(o_del + e_del * (i + 1)), gl);
+            E = gl < width ? enew : MINUS_INF_W;
+        } else {
+            Hd = h;
+            const int es = grp_shl1<G>(enew, MINUS_INF_W, gl);
+            E = gl + 1 < width ? es : MINUS_INF_W;
+            qv = grp_shl1<G>(qv, qn, gl);
+        }
+        beg = beg_next;
+        tb = tb_n;
+    }
+    const int hl = __shfl(h, width > 0 ? width - 1 : 0, G);
+    if (tlen > 0 && last_end == qlen) return hl;
+    return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
+}
+
+// bwa_gen_cigar2 for one group; sets dfr (and aligns nothing) when the band exceeds G columns or the
+// traceback matrix / target exceed the group's LDS slice
+template <int G>
+DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_off, int tcap, int z_off, int zcap,
+                     int qb, int l_query, int64_t rb, int64_t re, int *score, uint32_t *cig, int cap, int *ncig,
+                     bool &ovf, bool &dfr, uint64_t &cells, uint64_t &bases, int gl)
+{
+    *ncig = 0;
+    if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
+    const int64_t rlen = re - rb;
+    if (re > (ix.l_pac << 1) || rb < 0) return 0;
+    const bool rev = rb >= ix.l_pac;
+    const int q_start = rev ? qb + l_query - 1 : qb, q_dir = rev ? -1 : 1;
+    const int64_t t_start = rev ? re - 1 : rb;
+    const int t_dir = rev ? -1 : 1;
+    const Score sc = score_of(o);
+    if (l_query == rlen && w_ == 0) {
+        if (cap < 1) { ovf = true; return 0; }
+        bases += (uint64_t)((rlen + 3) >> 2);
+        cig[0] = (uint32_t)l_query << 4;
+        *ncig = 1;
+        int sum = 0;
+        for (int i = gl; i < l_query; i += G)
+            sum += sc(ref_at(ix, t_start + (int64_t)t_dir * i), g_lds_dp[q_off + q_start + q_dir * i]);
+        *score = grp_sum<G>(sum);
+        return 1;
+    }
+    int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
+    int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+    int max_gap = max_ins > max_del ? max_ins : max_del;
+    max_gap = max_gap > 1 ? max_gap : 1;
+    int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
+    int w = (max_gap + dl + 1) >> 1;
+    w = w < w_ ? w : w_;
+    const int min_w = dl + 3;
+    w = w > min_w ? w : min_w;
+    const int n_col = l_query < 2 * w + 1 ? l_query : 2 * w + 1;
+    if (n_col > G || rlen >= (int64_t)l_query + w || rlen > tcap || (int64_t)n_col * rlen > zcap || (o.exp_flags & 4)) {
+        dfr = true;
+        return 0;
+    }
+    bases += (uint64_t)((rlen + 3) >> 2);
+    for (int i = gl; i < (int)rlen; i += G) g_lds_dp[t_off + i] = (uint8_t)ref_at(ix, t_start + (int64_t)t_dir * i);
+    lds_fence();
+    *score = ksw_global2_g<G>(sc, l_query, q_off, q_start, q_dir, t_off, (int)rlen, o.o_del, o.e_del, o.o_ins,
+                              o.e_ins, w, n_col, z_off, cells, gl);
+    if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
+    traceback_w<true>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
+    return 1;
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) k_reg2aln_g(DIndex ix, DOpts o, Caps cp, const uint8_t *__restrict__ codes,
+                                                   const int64_t *__restrict__ offs, int n,
+                                                   const int32_t *__restrict__ list, const int32_t *__restrict__ list_n,
+                                                   const Reg *__restrict__ regs, const int32_t *__restrict__ n_regs,
+                                                   Hit *__restrict__ hits, uint32_t *__restrict__ cigars,
+                                                   int32_t *__restrict__ n_cig_read, uint32_t *__restrict__ status,
+                                                   int32_t *__restrict__ defer, int32_t *__restrict__ defer_n,
+                                                   Counters *ctr, int per_wave)
+{
+    constexpr int NG = 64 / G;
+    const int l = lane_id(), gl = l & (G - 1), grp = l / G;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int slice = (per_wave / NG) & ~15;
+    const int q_off = wave * per_wave + grp * slice;
+    const int qcap = (cp.max_len + 16) & ~15, tcap = (cp.max_len + 64 + 15) & ~15;
+    const int t_off = q_off + qcap, z_off = t_off + tcap;
+    const int zcap = slice - qcap - tcap;
+    const int n_items = list ? *list_n : n;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + wave, nw = gridDim.x * (blockDim.x >> 6);
+    uint64_t cells = 0, bases = 0;
+    for (int b = gw; b * NG < n_items; b += nw) {
+        const int k = b * NG + grp;
+        const int li = k < n_items ? (list ? list[k] : k) : -1;
+        if (li < 0) continue;
+        if (status[li]) { n_cig_read[li] = 0; continue; }
+        const uint8_t *q = codes + offs[li];
+        const int l_query = (int)(offs[li + 1] - offs[li]);
+        const int nr = n_regs[li];
+        for (int j = gl; j < l_query; j += G) g_lds_dp[q_off + j] = q[j];
+        lds_fence();
+        bool ovf = false, dfr = false;
+        int tot = 0;
+        for (int g = 0; g < nr && !ovf && !dfr; ++g) {
+            const Reg &ar = regs[(size_t)li * cp.regs + g];
+            uint32_t *cig = cigars + ((size_t)li * cp.regs + g) * cp.cigar;
+            const int qb = ar.qb, qe = ar.qe, truesc = ar.truesc;
+            const int64_t rb = ar.rb, re = ar.re;
+            const int flag = ar.secondary >= 0 ? 0x100 : 0;
+            int tmp = infer_bw(qe - qb, (int)(re - rb), truesc, o.a, o.o_del, o.e_del);
+            int w2 = infer_bw(qe - qb, (int)(re - rb), truesc, o.a, o.o_ins, o.e_ins);
+            w2 = w2 > tmp ? w2 : tmp;
+            if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
+            int i = 0, score = 0, last_sc = -(1 << 30), ncig = 0;
+            do {
+                w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+                gen_cigar2_g<G>(ix, o, w2, q_off, t_off, tcap, z_off, zcap, qb, qe - qb, rb, re, &score, cig,
+                                cp.cigar - 2, &ncig, ovf, dfr, cells, bases, gl);
+                if (ovf || dfr) break;
+                if (score == last_sc || w2 == o.w << 2) break;
+                last_sc = score;
+                w2 <<= 1;
+            } while (++i < 3 && score < truesc - o.a);
+            if (ovf || dfr) break;
+            int is_rev;
+            (void)depos(ix, rb < ix.l_pac ? rb : re - 1, is_rev);
+            if (ncig > 0) {
+                if ((cig[0] & 0xf) == 2) {
+                    --ncig;
+                    for (int t = 0; t < ncig; ++t) cig[t] = cig[t + 1];
+                } else if ((cig[ncig - 1] & 0xf) == 2) --ncig;
+            }
+            if (qb != 0 || qe != l_query) {
+                const int clip5 = is_rev ? l_query - qe : qb, clip3 = is_rev ? qb : l_query - qe;
+                if (clip5) {
+                    for (int t = ncig; t > 0; --t) cig[t] = cig[t - 1];
+                    cig[0] = (uint32_t)clip5 << 4 | 3;
+                    ++ncig;
+                }
+                if (clip3) cig[ncig++] = (uint32_t)clip3 << 4 | 3;
+            }
+            Hit hh;
+            hh.rb = rb; hh.re = re; hh.qb = qb; hh.qe = qe; hh.rid = ar.rid; hh.score = ar.score; hh.flag = flag;
+            hh.is_rev = is_rev; hh.n_cigar = ncig; hh.pad = 0;
+            hits[(size_t)li * cp.regs + g] = hh;
+            tot += ncig;
+        }
+        if (dfr) {
+            if (gl == 0) defer[atomicAdd(defer_n, 1)] = li;
+        } else if (ovf) {
+            if (gl == 0) status[li] |= ST_OVERFLOW;
+            n_cig_read[li] = 0;
+        } else n_cig_read[li] = tot;
+    }
+    if (gl != 0) { cells = 0; bases = 0; }   // group-uniform control: count once per group
+    wave_add(&ctr[STG_REG2ALN].dp_cells, cells);
+    wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
+}
+
+template <int G>
+static hipError_t launch_g(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                           const int64_t *offs, int n, const int32_t *list, const int32_t *list_n, const Reg *regs,
+                           const int32_t *n_regs, Hit *hits, uint32_t *cigars, int32_t *n_cig, uint32_t *status,
+                           int32_t *defer, int32_t *defer_n, Counters *ctr, int zcap, int max_blocks)
+{
+    const int waves = 4;
+    int grid = (n + waves * (64 / G) - 1) / (waves * (64 / G));
+    if (grid > max_blocks) grid = max_blocks;
+    if (grid == 0) return hipSuccess;
+    const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
+    const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
+    const size_t per_wave = eh_bytes + (size_t)zcap + q_bytes;
+    hipLaunchKernelGGL(k_reg2aln_g<G>, dim3(grid), dim3(64 * waves), waves * per_wave, st, ix, o, cp, codes, offs, n,
+                       list, list_n, regs, n_regs, hits, cigars, n_cig, status, defer, defer_n, ctr, (int)per_wave);
+    return hipGetLastError();
+}
+
+// group kernels G = 16 then 32 over the reads, the whole-wave kernel over what remains
+hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
+                                const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
+                                uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
+                                uint8_t *zslab, int64_t zslab_bytes, int max_blocks, int32_t *d0, int32_t *d1,
+                                int32_t *dn)
+{
+    hipError_t e = hipMemsetAsync(dn, 0, 2 * sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    e = launch_g<16>(st, ix, o, cp, codes, offs, n, nullptr, nullptr, regs, n_regs, hits, cigars, n_cig, status, d0,
+                     dn, ctr, zcap, max_blocks);
+    if (e != hipSuccess) return e;
+    e = launch_g<32>(st, ix, o, cp, codes, offs, n, d0, dn, regs, n_regs, hits, cigars, n_cig, status, d1, dn + 1, ctr,
+                     zcap, max_blocks);
+    if (e != hipSuccess) return e;
+    return launch_reg2aln_w(st, ix, o, cp, codes, offs, n, regs, n_regs, hits, cigars, n_cig, status, ctr, zcap, zslab,
+                            zslab_bytes, max_blocks, d1, dn + 1);
 }
 
 }  // namespace bsq
