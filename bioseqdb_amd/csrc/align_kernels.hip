@@ -12,6 +12,7 @@
 // Round-1 mapping: one read per lane (inter-task parallelism) with private scratch in HBM;
 // reads that overflow the small per-read slots are re-run by the host with large capacities.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "bsq_device.h"
@@ -1150,7 +1151,8 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
                                                            const int64_t *offs, const int32_t *sel, const int64_t *ids,
                                                            int n, const ChainDesc *chains, const Seed *seeds,
                                                            const int32_t *n_chains, Reg *regs_out, int32_t *n_regs,
-                                                           uint32_t *status, uint8_t *scratch, Counters *ctr)
+                                                           uint32_t *status, uint8_t *scratch, Counters *ctr,
+                                                           const int32_t *order)
 {
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1161,7 +1163,8 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
     X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
     X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
-    for (int li = tid; li < n; li += nthr) {
+    for (int it = tid; it < n; it += nthr) {
+        const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;
         if (status[li]) continue;
         const int r = read_of(sel, li);
@@ -1355,20 +1358,58 @@ hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts 
     return hipGetLastError();
 }
 
+// Per-read estimate of the extension DP work: the query bases outside each chain's longest seed,
+// summed over chains (ksw_extend2 runs ~one row per such base, per chain), as a sort key.
+__global__ void k_ext_key(const Caps cp, const int64_t *__restrict__ offs, const int32_t *__restrict__ sel, int n,
+                          const ChainDesc *__restrict__ chains, const Seed *__restrict__ seeds,
+                          const int32_t *__restrict__ n_chains, const uint32_t *__restrict__ status,
+                          uint32_t *__restrict__ key, int32_t *__restrict__ idx)
+{
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n) return;
+    uint32_t est = 0;
+    if (!status[li]) {
+        const int r = read_of(sel, li);
+        const int len = (int)(offs[r + 1] - offs[r]);
+        const ChainDesc *cd = chains + (size_t)li * cp.chains;
+        const Seed *sd = seeds + (size_t)li * cp.seeds;
+        const int nc = n_chains[li];
+        for (int c = 0; c < nc; ++c) {
+            int best = 0;
+            for (int k = 0; k < cd[c].n; ++k) best = best > sd[cd[c].seed_off + k].len ? best : sd[cd[c].seed_off + k].len;
+            est += (uint32_t)(len > best ? len - best : 0) + 4u;
+        }
+    }
+    key[li] = est < 65535u ? est : 65535u;
+    idx[li] = li;
+}
+
+hipError_t launch_ext_key(hipStream_t st, const Caps &cp, const int64_t *offs, const int32_t *sel, int n,
+                          const ChainDesc *chains, const Seed *seeds, const int32_t *n_chains, const uint32_t *status,
+                          uint32_t *key, int32_t *idx)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ext_key, dim3((n + 255) / 256), dim3(256), 0, st, cp, offs, sel, n, chains, seeds, n_chains,
+                       status, key, idx);
+    return hipGetLastError();
+}
+
 hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                          const int64_t *offs, const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
                          const Seed *seeds, const int32_t *n_chains, Reg *regs, int32_t *n_regs, uint32_t *status,
-                         uint8_t *scratch, Counters *ctr)
+                         uint8_t *scratch, Counters *ctr, const int32_t *order)
 {
     // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
-    const bool lds = cp.max_len <= 200 && (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
+    static const bool force_g = getenv("BSQ_EXT") && getenv("BSQ_EXT")[0] == 'g';   // timing experiments only
+    const bool lds = !force_g && cp.max_len <= 200 &&
+                     (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
         const size_t sh = (size_t)64 * (cp.max_len + 2) * 4 + (size_t)64 * (cp.max_len + 2);
         hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
-                           seeds, n_chains, regs, n_regs, status, scratch, ctr);
+                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order);
     } else {
         hipLaunchKernelGGL(k_extend<false>, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds,
-                           n_chains, regs, n_regs, status, scratch, ctr);
+                           n_chains, regs, n_regs, status, scratch, ctr, order);
     }
     return hipGetLastError();
 }

@@ -30,7 +30,9 @@ hipError_t launch_chain(int, hipStream_t, const DIndex &, const DOpts &, const C
                         Counters *);
 hipError_t launch_extend(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                          const int32_t *, const int64_t *, int, const ChainDesc *, const Seed *, const int32_t *, Reg *,
-                         int32_t *, uint32_t *, uint8_t *, Counters *);
+                         int32_t *, uint32_t *, uint8_t *, Counters *, const int32_t *);
+hipError_t launch_ext_key(hipStream_t, const Caps &, const int64_t *, const int32_t *, int, const ChainDesc *,
+                          const Seed *, const int32_t *, const uint32_t *, uint32_t *, int32_t *);
 hipError_t launch_reg2aln(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                           const int32_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *, uint32_t *,
                           uint8_t *, Counters *);
@@ -292,12 +294,17 @@ struct Workspace {
     int64_t zslab_bytes = 0;
     int zslab_blocks = 0;
     int32_t *dlist0 = nullptr, *dlist1 = nullptr, *dcount = nullptr;   // reads deferred by the group kernels
+    uint32_t *ekey0 = nullptr, *ekey1 = nullptr;   // extension work keys (main pass) and their sort
+    int32_t *eidx0 = nullptr, *eidx1 = nullptr;
+    void *esort_tmp = nullptr;
+    size_t esort_bytes = 0;
 
     void release()
     {
         hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
         hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
+        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp);
         *this = Workspace{};
     }
 };
@@ -342,6 +349,13 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
         HIPCHK(hipMalloc(&w.dcount, 16));
+        HIPCHK(hipMalloc(&w.ekey0, R * 4));
+        HIPCHK(hipMalloc(&w.ekey1, R * 4));
+        HIPCHK(hipMalloc(&w.eidx0, R * 4));
+        HIPCHK(hipMalloc(&w.eidx1, R * 4));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, w.esort_bytes, w.ekey0, w.ekey1, w.eidx0, w.eidx1, (int)R,
+                                                  0, 16));
+        HIPCHK(hipMalloc(&w.esort_tmp, std::max<size_t>(w.esort_bytes, 16)));
     }
     return BSQ_OK;
 }
@@ -545,8 +559,17 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, b->offs, sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
                         w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
+    const int32_t *order = nullptr;
+    static const bool no_sort = getenv("BSQ_EXT_SORT") && getenv("BSQ_EXT_SORT")[0] == '0';
+    if (!sel && w.ekey0 && n > 0 && !no_sort) {
+        // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
+        HIPCHK(launch_ext_key(st, w.cp, b->offs, sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
+        size_t tb = w.esort_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 16, st));
+        order = w.eidx1;
+    }
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, b->ids, n, w.chains, w.seeds, w.n_chains, w.regs,
-                         w.n_regs, w.status, w.scratch, b->ctr));
+                         w.n_regs, w.status, w.scratch, b->ctr, order));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
     if (!sel && w.cp.max_len <= 1024) {
         // main pass: one wave per read, DP rows across lanes, eh + traceback in LDS (dp_wave.hip)
