@@ -270,6 +270,22 @@ static uint64_t lrand48_state_at(uint64_t calls)
 }
 extern "C" int64_t bsq_lrand48_at(uint64_t pos) { return (int64_t)(lrand48_state_at(pos + 1) >> 17); }
 
+// ids[i] = the lrand48 value of call first + i (read i of the batch), by jump-ahead per read
+__global__ void k_lrand_ids(uint64_t first, int n, int64_t *ids)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t M = (1ULL << 48) - 1;
+    uint64_t C = 0, a = 0x5DEECE66DULL, c = 0xB, e = first + (uint64_t)i + 1;
+    while (e) {
+        if (e & 1) C = (a * C + c) & M;
+        c = (a * c + c) & M;
+        a = (a * a) & M;
+        e >>= 1;
+    }
+    ids[i] = (int64_t)(C >> 17);
+}
+
 // ================================================================================================
 // batch workspace
 // ================================================================================================
@@ -402,7 +418,9 @@ struct bsq_batch {
     int64_t out_cap = 0, out_cig_cap = 0;
     bsq_hit *h_pinned = nullptr;
     uint32_t *h_pinned_cig = nullptr;
-    int64_t h_cap = 0, h_cig_cap = 0;
+    int64_t *h_pinned_off = nullptr;
+    int64_t h_cap = 0, h_cig_cap = 0, h_off_cap = 0;
+    int64_t n_hits_main = 0, n_cig_main = 0;   // main-pass results left in the pinned buffers
     // results
     std::vector<bsq_hit> res_hits;
     std::vector<uint32_t> res_cig;
@@ -496,7 +514,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->codes); hipFree(b->offs); hipFree(b->ids); hipFree(b->ctr);
     hipFree(b->cnt_hits); hipFree(b->cnt_cig); hipFree(b->off_hits); hipFree(b->off_cig); hipFree(b->unresolved);
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
-    hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig);
+    hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
     delete b;
@@ -590,7 +608,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
 
 // Packs workspace w (n local reads) into host vectors hits/cig/off (hits with read_index = local).
 static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vector<bsq_hit> &hits,
-                        std::vector<uint32_t> &cig, std::vector<int64_t> &off, bool allow_unresolved)
+                        std::vector<uint32_t> &cig, std::vector<int64_t> &off, bool allow_unresolved,
+                        bool copy = true)
 {
     hipStream_t st = b->stream;
     SlotView v{w.hits, w.cigars, w.n_regs, w.n_cig, w.cp};
@@ -630,15 +649,24 @@ static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vect
     }
     const DeviceIndex *d = b->idx->h.dev;
     if (n && tot[0]) HIPCHK(launch_pack(st, n, v, v, nullptr, b->off_hits, b->off_cig, d->ann_off, d->ann_id, b->d_out, b->d_out_cig));
+    if ((int64_t)n + 1 > b->h_off_cap) {
+        hipHostFree(b->h_pinned_off);
+        b->h_off_cap = std::max<int64_t>((int64_t)n + 1, 2 * b->h_off_cap);
+        HIPCHK(hipHostMalloc((void **)&b->h_pinned_off, (size_t)b->h_off_cap * 8));
+    }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_D2H], st));
-    off.resize((size_t)n + 1);
-    HIPCHK(hipMemcpyAsync(off.data(), b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_pinned_off, b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
     if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
     if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_N], st));
     HIPCHK(hipStreamSynchronize(st));
-    hits.assign(b->h_pinned, b->h_pinned + tot[0]);
-    cig.assign(b->h_pinned_cig, b->h_pinned_cig + tot[1]);
+    b->n_hits_main = tot[0];
+    b->n_cig_main = tot[1];
+    if (copy) {   // otherwise the results stay in the pinned buffers (zero-copy view)
+        off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
+        hits.assign(b->h_pinned, b->h_pinned + tot[0]);
+        cig.assign(b->h_pinned_cig, b->h_pinned_cig + tot[1]);
+    }
     return BSQ_OK;
 }
 
@@ -657,19 +685,14 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     const int n = b->n_reads;
     const DOpts o = make_dopts(*opts);
     hipStream_t st = b->stream;
-    // lrand48 ids: read i consumes call first_call_seq + i
-    {
-        std::vector<int64_t> ids((size_t)std::max(n, 1));
-        const uint64_t M = (1ULL << 48) - 1;
-        uint64_t X = lrand48_state_at(first_call_seq);
-        for (int i = 0; i < n; ++i) { X = (0x5DEECE66DULL * X + 0xB) & M; ids[i] = (int64_t)(X >> 17); }
-        if (n) HIPCHK(hipMemcpyAsync(b->ids, ids.data(), (size_t)n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, st));
-        HIPCHK(hipStreamSynchronize(st));
-    }
+    // lrand48 ids: read i consumes call first_call_seq + i (computed on the device)
+    if (n) hipLaunchKernelGGL(k_lrand_ids, dim3((n + 255) / 256), dim3(256), 0, st, (uint64_t)first_call_seq, n, b->ids);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, st));
     b->retried = 0;
     b->res_hits.clear(); b->res_cig.clear(); b->res_off.assign((size_t)n + 1, 0);
     int rc = BSQ_OK;
+    bool zero_copy = false;
     if (n > 0 && b->idx->h.seq_len > 0) {
         rc = run_stages(b, b->main, o, n, nullptr, true);
         if (rc) return rc;
@@ -679,9 +702,14 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         int32_t novf = 0;
         HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true);
+        rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true, /*copy=*/false);
         if (rc) return rc;
+        zero_copy = novf == 0;
         if (novf > 0) {
+            // the retry pass reuses the pinned buffers: keep the main results first
+            b->res_off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
+            b->res_hits.assign(b->h_pinned, b->h_pinned + b->n_hits_main);
+            b->res_cig.assign(b->h_pinned_cig, b->h_pinned_cig + b->n_cig_main);
             b->retried = novf;
             std::vector<int32_t> list((size_t)novf);
             HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
@@ -754,7 +782,8 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_CHAIN] = 8.0 * c[STG_CHAIN].sa_values;
         b->stage_bytes[STG_EXTEND] = (double)c[STG_EXTEND].ref_bases;
         b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;
-        b->stage_bytes[STG_PACK] = (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
+        b->stage_bytes[STG_PACK] = zero_copy ? (double)b->n_hits_main * sizeof(bsq_hit) + 4.0 * b->n_cig_main
+                                             : (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks;
@@ -762,11 +791,19 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
     b->view.n_reads = n;
-    b->view.n_hits = (int64_t)b->res_hits.size();
-    b->view.hits = b->res_hits.data();
-    b->view.read_off = b->res_off.data();
-    b->view.n_cigar = (int64_t)b->res_cig.size();
-    b->view.cigar = b->res_cig.data();
+    if (zero_copy) {
+        b->view.n_hits = b->n_hits_main;
+        b->view.hits = b->h_pinned;
+        b->view.read_off = b->h_pinned_off;
+        b->view.n_cigar = b->n_cig_main;
+        b->view.cigar = b->h_pinned_cig;
+    } else {
+        b->view.n_hits = (int64_t)b->res_hits.size();
+        b->view.hits = b->res_hits.data();
+        b->view.read_off = b->res_off.data();
+        b->view.n_cigar = (int64_t)b->res_cig.size();
+        b->view.cigar = b->res_cig.data();
+    }
     return BSQ_OK;
 }
 
