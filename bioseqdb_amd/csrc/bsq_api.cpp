@@ -44,7 +44,10 @@ hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, con
 hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
 hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *,
                                 const int64_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *,
-                                uint32_t *, Counters *, int, uint8_t *, int64_t, int, int32_t *, int32_t *, int32_t *);
+                                uint32_t *, Counters *, int, uint8_t *, int64_t, int, int32_t *, int32_t *, int32_t *,
+                                const int32_t *, const int32_t *);
+hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
+                          const uint32_t *, uint32_t *, int32_t *, int32_t *);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int);
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
@@ -595,9 +598,18 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int64_t q_bytes = ((int64_t)w.cp.max_len + 16) & ~15LL;
         const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes - q_bytes) & ~15;
         // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
+        const int32_t *r_order = nullptr;
+        static const bool no_rsort = getenv("BSQ_R2A_SORT") && getenv("BSQ_R2A_SORT")[0] == '0';
+        if (w.ekey0 && !no_rsort) {
+            // group balance: reads in order of their band class (the extension's sort buffers are free now)
+            HIPCHK(launch_r2a_key(st, o, w.cp, b->offs, n, w.regs, w.n_regs, w.status, w.ekey0, w.eidx0, w.dcount + 2));
+            size_t tb = w.esort_bytes;
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 3, st));
+            r_order = w.eidx1;
+        }
         HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
                                     w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
-                                    w.dlist0, w.dlist1, w.dcount));
+                                    w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr));
     } else {
         HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars,
                               w.n_cig, w.status, w.scratch, b->ctr));

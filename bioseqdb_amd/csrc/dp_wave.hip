@@ -225,11 +225,16 @@ DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_
     return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
 }
 
-// traceback of a z matrix held in LDS (offset) or global memory; libbwa push_cigar semantics
-template <bool ZL>
+// traceback of a z matrix held in LDS (offset) or global memory; libbwa push_cigar semantics.
+// G lanes cooperate (a DPP row, a 32-lane segment or the wave; gl = lane in the group, gbase = the
+// group's first lane): in the match state the next G cells of the diagonal are read at once and a
+// ballot finds the first one whose state-0 transition leaves the diagonal, so a diagonal run of r
+// cells (mismatches included) is one push of r M's; other steps follow the serial loop exactly.
+template <bool ZL, int G>
 DEV void traceback_w(int qlen, int tlen, int w, int n_col, int z_off, const uint8_t *zg, uint32_t *cig, int cap,
-                     int *ncig, bool &ovf)
+                     int *ncig, bool &ovf, int gl = 0, int gbase = 0)
 {
+    if (G == 64) gl = lane_id();
     int n = 0, which = 0, i = tlen - 1;
     int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
     uint32_t cur = 0;
@@ -242,10 +247,24 @@ DEV void traceback_w(int qlen, int tlen, int w, int n_col, int z_off, const uint
         cur = (uint32_t)len << 4 | (uint32_t)op;
         ++n;
     };
+    auto zat = [&](int ii, int kk) -> int {
+        const int idx = ii * n_col + (kk - (ii > w ? ii - w : 0));
+        return ZL ? g_lds_dp[z_off + idx] : zg[idx];
+    };
     while (i >= 0 && k >= 0 && !ovf) {
-        const int idx = i * n_col + (k - (i > w ? i - w : 0));
-        const int zz = ZL ? g_lds_dp[z_off + idx] : zg[idx];
-        which = zz >> (which << 1) & 3;
+        if (which == 0) {
+            const int ii = i - gl, kk = k - gl;
+            const bool stop = ii < 0 || kk < 0 || (zat(ii, kk) & 3) != 0;
+            const uint64_t bal = __ballot(stop);
+            const uint64_t gm = G == 64 ? bal : (bal >> gbase) & ((1ull << G) - 1);
+            const int r = gm ? (int)__builtin_ctzll(gm) : G;
+            if (r > 0) {
+                push(0, r);
+                i -= r; k -= r;
+                continue;
+            }
+        }
+        which = zat(i, k) >> (which << 1) & 3;
         if (which == 0) push(0, 1), --i, --k;
         else if (which == 1) push(2, 1), --i;
         else push(1, 1), --k;
@@ -301,8 +320,8 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
                         : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
                                                  (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
             if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
-            if (zl) traceback_w<true>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
-            else traceback_w<false>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
+            if (zl) traceback_w<true, 64>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
+            else traceback_w<false, 64>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
         } else {
             *score = ksw_global2_w(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, z, zcap,
                                    cig, cap, ncig, ovf, cells);
@@ -582,7 +601,7 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
     *score = ksw_global2_g<G>(sc, l_query, q_off, q_start, q_dir, t_off, (int)rlen, o.o_del, o.e_del, o.o_ins,
                               o.e_ins, w, n_col, z_off, cells, gl);
     if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
-    traceback_w<true>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
+    traceback_w<true, G>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf, gl, lane_id() & ~(G - 1));
     return 1;
 }
 
@@ -693,16 +712,65 @@ static hipError_t launch_g(hipStream_t st, const DIndex &ix, const DOpts &o, con
     return hipGetLastError();
 }
 
-// group kernels G = 16 then 32 over the reads, the whole-wave kernel over what remains
+// Sort key of a read for mem_reg2aln: the widest first-iteration band class over its regions
+// (0: exact, no DP; 1: <= 16 columns; 2: <= 32; 3: <= 64; 4: wider), so each group-mode wave holds
+// reads of one class.  Only the processing order depends on it.
+__global__ void k_r2a_key(DOpts o, Caps cp, const int64_t *__restrict__ offs, int n, const Reg *__restrict__ regs,
+                          const int32_t *__restrict__ n_regs, const uint32_t *__restrict__ status,
+                          uint32_t *__restrict__ key, int32_t *__restrict__ idx, int32_t *__restrict__ n_out)
+{
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li == 0) *n_out = n;
+    if (li >= n) return;
+    uint32_t cls = 0;
+    if (!status[li]) {
+        const int nr = n_regs[li];
+        for (int g = 0; g < nr; ++g) {
+            const Reg &ar = regs[(size_t)li * cp.regs + g];
+            const int lq = ar.qe - ar.qb;
+            const int64_t rl = ar.re - ar.rb;
+            int tmp = infer_bw(lq, (int)rl, ar.truesc, o.a, o.o_del, o.e_del);
+            int w2 = infer_bw(lq, (int)rl, ar.truesc, o.a, o.o_ins, o.e_ins);
+            w2 = w2 > tmp ? w2 : tmp;
+            if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
+            w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+            uint32_t c;
+            if (lq == rl && w2 == 0) c = 0;
+            else {
+                int mg = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
+                int md = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+                mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
+                int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
+                int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
+                const int nc = lq < 2 * ww + 1 ? lq : 2 * ww + 1;
+                c = nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 3 : 4;
+            }
+            cls = cls > c ? cls : c;
+        }
+    }
+    key[li] = cls;
+    idx[li] = li;
+}
+
+hipError_t launch_r2a_key(hipStream_t st, const DOpts &o, const Caps &cp, const int64_t *offs, int n, const Reg *regs,
+                          const int32_t *n_regs, const uint32_t *status, uint32_t *key, int32_t *idx, int32_t *n_out)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_r2a_key, dim3((n + 255) / 256), dim3(256), 0, st, o, cp, offs, n, regs, n_regs, status, key,
+                       idx, n_out);
+    return hipGetLastError();
+}
+
+// group kernels G = 16 then 32 over the reads (in `order` when given), the whole-wave kernel over what remains
 hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                                 const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
                                 uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
                                 uint8_t *zslab, int64_t zslab_bytes, int max_blocks, int32_t *d0, int32_t *d1,
-                                int32_t *dn)
+                                int32_t *dn, const int32_t *order, const int32_t *order_n)
 {
     hipError_t e = hipMemsetAsync(dn, 0, 2 * sizeof(int32_t), st);
     if (e != hipSuccess) return e;
-    e = launch_g<16>(st, ix, o, cp, codes, offs, n, nullptr, nullptr, regs, n_regs, hits, cigars, n_cig, status, d0,
+    e = launch_g<16>(st, ix, o, cp, codes, offs, n, order, order_n, regs, n_regs, hits, cigars, n_cig, status, d0,
                      dn, ctr, zcap, max_blocks);
     if (e != hipSuccess) return e;
     e = launch_g<32>(st, ix, o, cp, codes, offs, n, d0, dn, regs, n_regs, hits, cigars, n_cig, status, d1, dn + 1, ctr,
