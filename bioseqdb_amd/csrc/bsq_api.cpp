@@ -565,7 +565,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
-        const int lcap = tiny_caps() ? 3 : ix.seq_len < 0xFFFFFFFFull ? 28 : 16;
+        static const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning experiments
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : ix.seq_len < 0xFFFFFFFFull ? 20 : 16;
         static const char *alt = getenv("BSQ_SMEM");
         static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
         if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)
