@@ -10,8 +10,10 @@ Usage: traffic_from_pmc.py <profile dir> <out json> <round tag>
 """
 import csv, glob, json, os, sys
 
-KERNELS = {"smem": "k_smem_lds<unsigned int>", "chain": "bsq::k_chain", "extend": "k_extend<true>",
-           "reg2aln": "bsq::k_reg2aln_w"}
+# stage -> kernels its HIP events bracket (the sorts' rocprim kernels are negligible and not counted)
+KERNELS = {"smem": ["k_smem_lds<unsigned int>"], "chain": ["bsq::k_chain"],
+           "extend": ["k_ext_key", "k_extend<true>"],
+           "reg2aln": ["k_r2a_key", "k_reg2aln_g<16>", "k_reg2aln_g<32>", "bsq::k_reg2aln_w"]}
 
 
 def per_dispatch(d, counter):
@@ -36,15 +38,20 @@ def main(root, dst, tag):
     fetch, write = per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE"), per_dispatch(os.path.join(root, "write"), "WRITE_SIZE")
     res = {"round": tag, "reads_per_launch": 1000000, "fetch_correction": 1.0 / corr,
            "calibration_fetch_size_over_bytes": calib, "kernels": {}}
-    for stage, pat in KERNELS.items():
-        fk = [k for k in fetch if pat in k]
-        wk = [k for k in write if pat in k]
-        if not fk or not wk:
-            continue
-        fb = sum(fetch[fk[0]]) / len(fetch[fk[0]])
-        wb = sum(write[wk[0]]) / len(write[wk[0]])
-        res["kernels"][stage] = {"kernel": fk[0].split("(")[0], "fetch_bytes": fb / corr, "write_bytes": wb,
-                                 "traffic_bytes": fb / corr + wb}
+    for stage, pats in KERNELS.items():
+        fb = wb = 0.0
+        names = []
+        for pat in pats:
+            fk = [k for k in fetch if pat in k]
+            wk = [k for k in write if pat in k]
+            if not fk or not wk:
+                continue
+            fb += sum(fetch[fk[0]]) / len(fetch[fk[0]])
+            wb += sum(write[wk[0]]) / len(write[wk[0]])
+            names.append(fk[0].split("(")[0])
+        if names:
+            res["kernels"][stage] = {"kernel": " + ".join(names), "fetch_bytes": fb / corr, "write_bytes": wb,
+                                     "traffic_bytes": fb / corr + wb}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
