@@ -91,17 +91,28 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    gpu = local
+    xdev = None   # device of the exchange tensors
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()   # does not initialise the GPU
+        gpu = local % max(ndev, 1)         # one GPU per rank; several ranks share one only in a gloo rehearsal
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            xdev = torch.device("cuda", gpu)
+            dist.init_process_group("nccl", device_id=xdev)
+        else:
+            xdev = torch.device("cpu")
+            dist.init_process_group("gloo")
     L = N.lib()
     t0 = time.time()
     ref = synth.make_reference(args.ref_bp)
@@ -123,7 +134,7 @@ def main() -> int:
     N.check(L.bsq_index_build(idx, 0))
     t_build = time.time() - t0
     t0 = time.time()
-    N.check(L.bsq_index_upload(idx, local))
+    N.check(L.bsq_index_upload(idx, gpu))
     t_upload = time.time() - t0
     opts = default_opts(len(ref.rows))
 
@@ -147,7 +158,7 @@ def main() -> int:
             nc = H.n_cigar * 4
             hb = np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb]
             cb = np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc]
-            D.gather_records(np.concatenate([hb, cb]), device=torch.device("cuda", local))
+            D.gather_records(np.concatenate([hb, cb]), device=xdev)
 
     for _ in range(args.warmup):
         step()
@@ -177,7 +188,7 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stage_ms /= max(args.steps, 1)

@@ -3,7 +3,7 @@
 The SQL path is embarrassingly parallel over query rows (extension.cpp:362-370 aligns one cursor row
 at a time and libbwa keeps no cross-read state except the lrand48 position, Q10).  Each rank takes a
 contiguous slice of the reads, aligns it on its own GPU against its own replica of the index, and the
-hit records travel to rank 0 (the calling backend) in one all-gather, which preserves read order
+hit records travel to rank 0 (the calling backend) in one gather, which preserves read order
 (rank order == read order, Q16).  No other collective sits on the data path.
 """
 from __future__ import annotations
@@ -23,15 +23,17 @@ def first_call_of(rank: int, world: int, n_total: int, base: int = 0) -> int:
     return base + shard(n_total, rank, world)[0]
 
 
-def gather_records(local: np.ndarray, group=None, device=None) -> List[np.ndarray]:
-    """All-gather variable-length uint8 record buffers; returns them in rank order (valid on every rank).
+def gather_records(local: np.ndarray, group=None, device=None, dst: int = 0) -> List[np.ndarray]:
+    """Gather variable-length uint8 record buffers to rank `dst` (the calling backend), in rank order.
 
-    Works with the "nccl" (RCCL, tensors on `device`) and "gloo" (CPU tensors) backends: one
-    all-gather of the byte counts, one all-gather of the buffers padded to the largest."""
+    Returns the per-rank buffers on `dst` and [] elsewhere.  Works with the "nccl" (RCCL, tensors on
+    `device`) and "gloo" (CPU tensors) backends: one all-gather of the byte counts, one gather of the
+    buffers padded to the largest -- only the caller receives rows, as in the SQL path."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    me = dist.get_rank(group)
     dev = device if device is not None else torch.device("cpu")
     n = torch.tensor([local.nbytes], dtype=torch.int64, device=dev)
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
@@ -41,8 +43,10 @@ def gather_records(local: np.ndarray, group=None, device=None) -> List[np.ndarra
     buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
     if local.nbytes:
         buf[:local.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(local).view(np.uint8).reshape(-1)))
-    out = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
-    dist.all_gather(out, buf, group=group)
+    out = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if me == dst else None
+    dist.gather(buf, out, dst=dst, group=group)
+    if me != dst:
+        return []
     return [o[:s].cpu().numpy() for o, s in zip(out, sizes_i)]
 
 

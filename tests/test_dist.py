@@ -51,7 +51,10 @@ def test_gather_records_world2_gloo():
     res.sort()
     locals_ = [r[2] for r in res]
     for rank, got, _ in res:
-        assert got == locals_, rank           # every rank sees all records in rank (= read) order
+        if rank == 0:
+            assert got == locals_, rank       # the caller sees every rank's records in rank (= read) order
+        else:
+            assert got == [], rank            # only the calling backend receives rows
 
 
 def test_merge_rows():
