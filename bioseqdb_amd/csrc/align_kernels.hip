@@ -13,6 +13,7 @@
 // reads that overflow the small per-read slots are re-run by the host with large capacities.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <algorithm>
 #include <stdint.h>
 
 #include "bsq_device.h"
@@ -643,15 +644,31 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
 // ksw_extend2 keeps h and e in [0, h0 + qlen*max] (every candidate is clamped at 0), so u16 is exact
 // whenever the host-side bound check passes.
 struct EhG {
+    static constexpr bool kRing = false;
     int2 *p;
+    bool *ovf = nullptr;
     DEV int2 get(int j) const { return p[j]; }
     DEV void set(int j, int2 v) const { p[j] = v; }
 };
 extern __shared__ uint32_t g_lds_eh[];   // dynamic LDS of k_extend<true>
 struct EhL {   // offset-based so the accesses stay in the LDS address space (ds_read/ds_write, not flat)
+    static constexpr bool kRing = false;
     int base;
+    bool *ovf = nullptr;
     DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + j * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
     DEV void set(int j, int2 v) const { g_lds_eh[base + j * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
+};
+
+// 64-column ring of u16 pairs in LDS (column j at slot j & 63, lane-interleaved): ksw_extend2 only touches
+// columns [beg, end] of the current row and beg never decreases, so the ring holds every live column while
+// the window stays under 64 columns; columns are given their initial value when the band first reaches
+// them.  A wider window sets *ovf (the read is re-run by the large-capacity retry pass).
+struct EhRing {
+    static constexpr bool kRing = true;
+    bool *ovf;
+    int base;
+    DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + (j & 63) * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
+    DEV void set(int j, int2 v) const { g_lds_eh[base + (j & 63) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
 template <class EH, class QA>
@@ -664,13 +681,11 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, 
     if (o.exp_flags & 1) { *_qle = *_tle = *_gtle = 0; *_gscore = -1; *_max_off = 0; return h0; }
     const Score sc = score_of(o);
     if (qlen < 0) qlen = 0;
-    {   // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
-        const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
-        for (j = 0; j <= qlen; ++j) {
-            int h = j == 0 ? h0 : (j == 1 ? v1 : (v1 - (j - 1) * e_ins > 0 ? v1 - (j - 1) * e_ins : 0));
-            eh.set(j, make_int2(h, 0));
-        }
-    }
+    // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
+    const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+    auto init_h = [&](int jj) { return jj == 0 ? h0 : (jj == 1 ? v1 : (v1 - (jj - 1) * e_ins > 0 ? v1 - (jj - 1) * e_ins : 0)); };
+    int hi = EH::kRing ? (qlen < 63 ? qlen : 63) : qlen;   // columns <= hi hold their values
+    for (j = 0; j <= hi; ++j) eh.set(j, make_int2(init_h(j), 0));
     max = o.mat_max > 0 ? o.mat_max : 0;
     max_ins = (int)((double)(qlen * max + end_bonus - o_ins) / e_ins + 1.);
     max_ins = max_ins > 1 ? max_ins : 1;
@@ -693,6 +708,11 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, 
             h1 = h0 - (o_del + e_del * (i + 1));
             if (h1 < 0) h1 = 0;
         } else h1 = 0;
+        if (EH::kRing && end > hi) {   // materialise the columns the band reaches for the first time
+            if (end - beg >= 63) { *eh.ovf = true; break; }
+            for (j = hi + 1; j <= end; ++j) eh.set(j, make_int2(init_h(j), 0));
+            hi = end;
+        }
         cells += (uint64_t)(end > beg ? end - beg : 0);
         for (j = beg; j < end; ++j) {
             int2 p = eh.get(j);
@@ -901,6 +921,31 @@ struct QMakeL {
     DEV QLane at(int start, int dir) const { return QLane{off, start, dir}; }
 };
 
+// Extension rows for k_extend<true>: the eh row is a 64-column LDS ring (EhRing); the read is staged
+// in LDS once per read (QMakeL) after the ring columns.
+#define EXT_LDS_COLS 64
+struct EhSmall {
+    int lane;       // LDS column (threadIdx.x of the 64-thread block)
+    bool *ovf;      // ring overflow -> read re-run by the retry pass
+};
+
+template <class QA>
+DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins, int e_ins,
+                 int w, int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore, int *max_off,
+                 EhSmall ehx, uint64_t &cells)
+{
+    return ksw_extend2(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, qle, tle, gtle,
+                       gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
+}
+template <class QA, class EH>
+DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins, int e_ins,
+                 int w, int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore, int *max_off,
+                 EH ehx, uint64_t &cells)
+{
+    return ksw_extend2(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, qle, tle, gtle,
+                       gscore, max_off, ehx, cells);
+}
+
 template <class EH, class QM>
 DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
                    ExtCtx &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
@@ -981,7 +1026,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
             for (int t = 0; t < 2; ++t) {
                 int prev = a.score;
                 aw0 = o.w << t;
-                a.score = ksw_extend2(o, s.qbeg, qa, (int)tmp, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, aw0, o.pen_clip5,
+                a.score = ext_call(o, s.qbeg, qa, (int)tmp, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, aw0, o.pen_clip5,
                                       o.zdrop, s.len * o.a, &qle, &tle, &gtle, &gscore, &max_off0, ehx, cells);
                 if (a.score == prev || max_off0 < (aw0 >> 1) + (aw0 >> 2)) break;
             }
@@ -1002,7 +1047,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
             for (int t = 0; t < 2; ++t) {
                 int prev = a.score;
                 aw1 = o.w << t;
-                a.score = ksw_extend2(o, l_query - qe, qa, (int)(rmax1 - rmax0 - re), ta, o.o_del, o.e_del, o.o_ins,
+                a.score = ext_call(o, l_query - qe, qa, (int)(rmax1 - rmax0 - re), ta, o.o_del, o.e_del, o.o_ins,
                                       o.e_ins, aw1, o.pen_clip3, o.zdrop, sc0, &qle, &tle, &gtle, &gscore, &max_off1,
                                       ehx, cells);
                 if (a.score == prev || max_off1 < (aw1 >> 1) + (aw1 >> 2)) break;
@@ -1176,8 +1221,8 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
         const Seed *sd = seeds + (size_t)li * cp.seeds;
         const int nc = n_chains[li];
         if (LDS) {
-            EhL ehx{(int)threadIdx.x};   // blockDim == 64: lane-interleaved u16 pairs
-            const int qoff = 64 * (cp.max_len + 2) * 4 + (int)threadIdx.x;
+            EhSmall ehx{(int)threadIdx.x, &X.ovf};   // blockDim == 64: lane-interleaved LDS columns
+            const int qoff = 64 * EXT_LDS_COLS * 4 + (int)threadIdx.x;
             for (int j = 0; j < len; ++j) g_lds_q8[qoff + j * 64] = q[j];   // stage the read in LDS
             QMakeL qm{qoff};
             for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
@@ -1404,7 +1449,8 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     const bool lds = !force_g && cp.max_len <= 200 &&
                      (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
-        const size_t sh = (size_t)64 * (cp.max_len + 2) * 4 + (size_t)64 * (cp.max_len + 2);
+        static const size_t sh_env = getenv("BSQ_EXT_SH") ? (size_t)atol(getenv("BSQ_EXT_SH")) : 0;   // tuning only
+        const size_t sh = std::max((size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2), sh_env);
         hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
                            seeds, n_chains, regs, n_regs, status, scratch, ctr, order);
     } else {
