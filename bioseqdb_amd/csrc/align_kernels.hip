@@ -65,7 +65,7 @@ DEV void bwt_extend(const DIndex &ix, const Intv &ik, Intv ok[4], int is_back, u
     occ4(ix, l, tl);
     {
         uint64_t kk = k == (uint64_t)-1 ? k : k - (k >= ix.primary), ll = l - (l >= ix.primary);
-        nblk += (k == (uint64_t)-1 || (kk >> 7) == (ll >> 7)) ? 1 : 2;
+        nblk += (k == (uint64_t)-1 || (kk >> 7) == (ll >> 7)) ? 2 : 4;   // 32-B units
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -114,11 +114,12 @@ struct DeviceIndex {
     int64_t *ann_off = nullptr, *ann_id = nullptr;
     int32_t *ann_len = nullptr;
     uint32_t *kmer = nullptr;
+    OccBlock32 *occ32 = nullptr;
     DIndex view{};
     ~DeviceIndex()
     {
         if (device >= 0) hipSetDevice(device);
-        hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len); hipFree(kmer);
+        hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len); hipFree(kmer); hipFree(occ32);
     }
 };
 }  // namespace bsq
@@ -238,6 +239,26 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
     v.l_pac = h.l_pac;
     v.kmer = nullptr;
     v.kmer_k = 0;
+    v.occ32 = nullptr;
+    if (h.seq_len > 0 && h.seq_len < 0xFFFFFFFFull) {
+        // 64-base blocks: half 0 of each 128-base block keeps its counts, half 1 adds the first 64 bases
+        std::vector<OccBlock32> o32(h.occ.size() * 2);
+        for (size_t b = 0; b < h.occ.size(); ++b) {
+            const OccBlock &B = h.occ[b];
+            const uint64_t hi = B.hi[0], lo = B.lo[0];
+            const uint32_t n3 = (uint32_t)__builtin_popcountll(hi & lo), n2 = (uint32_t)__builtin_popcountll(hi & ~lo);
+            const uint32_t n1 = (uint32_t)__builtin_popcountll(~hi & lo), n0 = 64u - n1 - n2 - n3;
+            OccBlock32 &a = o32[2 * b], &c = o32[2 * b + 1];
+            for (int t = 0; t < 4; ++t) a.cnt[t] = (uint32_t)B.cnt[t];
+            a.hi = B.hi[0]; a.lo = B.lo[0];
+            c.cnt[0] = (uint32_t)B.cnt[0] + n0; c.cnt[1] = (uint32_t)B.cnt[1] + n1;
+            c.cnt[2] = (uint32_t)B.cnt[2] + n2; c.cnt[3] = (uint32_t)B.cnt[3] + n3;
+            c.hi = B.hi[1]; c.lo = B.lo[1];
+        }
+        HIPCHK(hipMalloc(&d->occ32, o32.size() * sizeof(OccBlock32)));
+        HIPCHK(hipMemcpy(d->occ32, o32.data(), o32.size() * sizeof(OccBlock32), hipMemcpyHostToDevice));
+        v.occ32 = d->occ32;
+    }
     // k-mer interval table (u32 rows): depth ~log4(rows), at most 11 (89 MB, stays in the Infinity
     // Cache beside the occ array at 100 Mbp); BSQ_KMER_K overrides, 0 disables
     if (h.seq_len > 0 && h.seq_len < 0xFFFFFFFFull) {
@@ -791,7 +812,7 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         Counters c[STG_N];
         HIPCHK(hipMemcpy(c, b->ctr, sizeof c, hipMemcpyDeviceToHost));
         b->stage_bytes[STG_SMEM] =
-            64.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
+            32.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
         b->stage_bytes[STG_CHAIN] = 8.0 * c[STG_CHAIN].sa_values;
         b->stage_bytes[STG_EXTEND] = (double)c[STG_EXTEND].ref_bases;
         b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;
@@ -799,7 +820,7 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
                                              : (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
-        b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks;
+        b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
     } else {
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }

@@ -15,6 +15,15 @@ struct alignas(64) OccBlock {
 };
 static_assert(sizeof(OccBlock) == 64, "occ block must be one 64-byte sector");
 
+// Half-size rank block for texts with < 2^32 rows: u32 counts before the block + the two bit-planes
+// of 64 bases, 32 bytes.  Same 0.5 B/base as OccBlock, but a rank query popcounts one 64-bit word per
+// plane instead of two.  Derived from OccBlock at upload (bsq_api.cpp) and used by the seeding kernels.
+struct alignas(32) OccBlock32 {
+    uint32_t cnt[4];
+    uint64_t hi, lo;
+};
+static_assert(sizeof(OccBlock32) == 32, "occ32 block must be 32 bytes");
+
 // Device view of the index (passed by value as a kernel argument).
 struct DIndex {
     const OccBlock *occ;
@@ -32,6 +41,7 @@ struct DIndex {
     // interval (x[0], x[1], x[2], 0) that bwt_extend chains produce for S (u32 rows only), at entry
     // (4^|S| - 4)/3 + code(S), code = base-4 value of S with the first base most significant
     const uint32_t *kmer;
+    const OccBlock32 *occ32;  // 64-base rank blocks (u32 rows only; nullptr otherwise)
 };
 
 // mem_opt_t fields the path reads (mem_opt_init defaults + bioseqdb overrides).
@@ -76,7 +86,7 @@ enum Stage { STG_SMEM = 0, STG_CHAIN, STG_EXTEND, STG_REG2ALN, STG_PACK, STG_D2H
 
 // device-side algorithmic byte counters, one slot per stage
 struct Counters {
-    unsigned long long occ_blocks;   // 64-B occ block fetches in bwt_extend
+    unsigned long long occ_blocks;   // occ block fetches in bwt_extend, in 32-B units (a 64-B OccBlock counts 2)
     unsigned long long sa_values;    // SA values produced
     unsigned long long ref_bases;    // reference bases fetched for extension / CIGAR
     unsigned long long dp_cells;     // DP cells evaluated (secondary figure)

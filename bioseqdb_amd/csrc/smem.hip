@@ -23,6 +23,7 @@ namespace bsq {
 template <typename X>
 struct FM {
     const OccBlock *occ;
+    const OccBlock32 *occ32;   // 64-base blocks, used when X is u32
     const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
     int K;
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
@@ -60,6 +61,23 @@ DEV void occ_c(const uint4 (&w)[4], X k, bool none, int c, X &cc, X &cg)
     cg = ((b1 & s0) + (b2 & (s0 | s1)) + (b3 & (s0 | s1 | s2)) + ng) & live;
 }
 
+// The same two sums from a 64-base OccBlock32 (w[0] = counts, w[1] = hi/lo planes): one word per plane.
+DEV void occ_c32(const uint4 (&w)[2], uint32_t k, bool none, int c, uint32_t &cc, uint32_t &cg)
+{
+    const uint32_t r = (k & 63) + 1;
+    const uint64_t h = (uint64_t)w[1].y << 32 | w[1].x, l = (uint64_t)w[1].w << 32 | w[1].z;
+    const uint64_t m = r >= 64 ? ~0ull : ((1ull << r) - 1);
+    const uint64_t fh = (c & 2) ? 0ull : ~0ull, fl = (c & 1) ? 0ull : ~0ull;
+    const uint64_t any = c == 0 ? ~0ull : 0ull;
+    const uint64_t ah = c < 2 ? ~0ull : (c == 2 ? l : 0ull);
+    const uint32_t nc = __popcll((h ^ fh) & (l ^ fl) & m);
+    const uint32_t ng = __popcll(((h & ah) | (l & any)) & m);
+    const uint32_t live = none ? 0u : ~0u;
+    const uint32_t s0 = -(uint32_t)(c == 0), s1 = -(uint32_t)(c == 1), s2 = -(uint32_t)(c == 2), s3 = -(uint32_t)(c == 3);
+    cc = (((w[0].x & s0) | (w[0].y & s1) | (w[0].z & s2) | (w[0].w & s3)) + nc) & live;
+    cg = ((w[0].y & s0) + (w[0].z & (s0 | s1)) + (w[0].w & (s0 | s1 | s2)) + ng) & live;
+}
+
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
 // used for the rank queries (x[1] forward, x[0] backward), `o` the other one.
 template <typename X>
@@ -68,15 +86,26 @@ DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, u
     const X k = a - 1, l = a - 1 + x2;
     const bool knone = k == (X)-1;
     const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-    const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ + (knone ? 0 : (kk >> 7)));
-    const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ + (ll >> 7));
-    uint4 wk[4], wl[4];
-    wk[0] = pk[0]; wk[1] = pk[1]; wk[2] = pk[2]; wk[3] = pk[3];
-    wl[0] = pl[0]; wl[1] = pl[1]; wl[2] = pl[2]; wl[3] = pl[3];
     X kc, kg, lc, lg;
-    occ_c(wk, kk, knone, c, kc, kg);
-    occ_c(wl, ll, false, c, lc, lg);
-    nblk += (knone || (kk >> 7) == (ll >> 7)) ? 1 : 2;
+    if constexpr (sizeof(X) == 4) {
+        const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ32 + (knone ? 0 : (kk >> 6)));
+        const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ32 + (ll >> 6));
+        uint4 wk[2], wl[2];
+        wk[0] = pk[0]; wk[1] = pk[1];
+        wl[0] = pl[0]; wl[1] = pl[1];
+        occ_c32(wk, kk, knone, c, kc, kg);
+        occ_c32(wl, ll, false, c, lc, lg);
+        nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
+    } else {
+        const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ + (knone ? 0 : (kk >> 7)));
+        const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ + (ll >> 7));
+        uint4 wk[4], wl[4];
+        wk[0] = pk[0]; wk[1] = pk[1]; wk[2] = pk[2]; wk[3] = pk[3];
+        wl[0] = pl[0]; wl[1] = pl[1]; wl[2] = pl[2]; wl[3] = pl[3];
+        occ_c(wk, kk, knone, c, kc, kg);
+        occ_c(wl, ll, false, c, lc, lg);
+        nblk += (knone || (kk >> 7) == (ll >> 7)) ? 2 : 4;
+    }
     na = fm.L2(c) + 1 + kc;
     nx2 = lc - kc;
     no = o + (X)(a <= fm.primary && a + x2 - 1 >= fm.primary) + (lg - kg);
@@ -93,30 +122,50 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
     const bool kan = ka == (X)-1, kbn = kb == (X)-1;
     const X kka = ka - (ka >= fm.primary), lla = la - (la >= fm.primary);
     const X kkb = kb - (kb >= fm.primary), llb = lb - (lb >= fm.primary);
-    const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ + (kan ? 0 : (kka >> 7)));
-    const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ + (lla >> 7));
-    const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ + (kbn ? 0 : (kkb >> 7)));
-    const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ + (llb >> 7));
-    uint4 w0[4], w1[4], w2[4], w3[4];
-    if (da) {
-        w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
-        w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
-    }
-    if (hb) {
-        w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
-        w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
-    }
     X kc, kg, lc, lg;
-    occ_c(w0, kka, kan, c, kc, kg);
-    occ_c(w1, lla, false, c, lc, lg);
-    ra0 = fm.L2(c) + 1 + kc;
-    ra2 = lc - kc;
-    occ_c(w2, kkb, kbn, c, kc, kg);
-    occ_c(w3, llb, false, c, lc, lg);
-    rb0 = fm.L2(c) + 1 + kc;
-    rb2 = lc - kc;
-    if (da) nblk += (kan || (kka >> 7) == (lla >> 7)) ? 1 : 2;
-    if (hb) nblk += (kbn || (kkb >> 7) == (llb >> 7)) ? 1 : 2;
+    if constexpr (sizeof(X) == 4) {
+        const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ32 + (kan ? 0 : (kka >> 6)));
+        const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ32 + (lla >> 6));
+        const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ32 + (kbn ? 0 : (kkb >> 6)));
+        const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ32 + (llb >> 6));
+        uint4 w0[2], w1[2], w2[2], w3[2];
+        if (da) { w0[0] = p0[0]; w0[1] = p0[1]; w1[0] = p1[0]; w1[1] = p1[1]; }
+        if (hb) { w2[0] = p2[0]; w2[1] = p2[1]; w3[0] = p3[0]; w3[1] = p3[1]; }
+        occ_c32(w0, kka, kan, c, kc, kg);
+        occ_c32(w1, lla, false, c, lc, lg);
+        ra0 = fm.L2(c) + 1 + kc;
+        ra2 = lc - kc;
+        occ_c32(w2, kkb, kbn, c, kc, kg);
+        occ_c32(w3, llb, false, c, lc, lg);
+        rb0 = fm.L2(c) + 1 + kc;
+        rb2 = lc - kc;
+        if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
+        if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
+    } else {
+        const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ + (kan ? 0 : (kka >> 7)));
+        const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ + (lla >> 7));
+        const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ + (kbn ? 0 : (kkb >> 7)));
+        const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ + (llb >> 7));
+        uint4 w0[4], w1[4], w2[4], w3[4];
+        if (da) {
+            w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
+            w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
+        }
+        if (hb) {
+            w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
+            w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
+        }
+        occ_c(w0, kka, kan, c, kc, kg);
+        occ_c(w1, lla, false, c, lc, lg);
+        ra0 = fm.L2(c) + 1 + kc;
+        ra2 = lc - kc;
+        occ_c(w2, kkb, kbn, c, kc, kg);
+        occ_c(w3, llb, false, c, lc, lg);
+        rb0 = fm.L2(c) + 1 + kc;
+        rb2 = lc - kc;
+        if (da) nblk += (kan || (kka >> 7) == (lla >> 7)) ? 2 : 4;
+        if (hb) nblk += (kbn || (kkb >> 7) == (llb >> 7)) ? 2 : 4;
+    }
 }
 
 // first entry of the k-mer table level for strings of length L: (4^L - 4) / 3
@@ -296,6 +345,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     L.cap = lcap;
     FM<X> fm;
     fm.occ = ix.occ;
+    fm.occ32 = ix.occ32;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
@@ -420,6 +470,7 @@ __global__ void __launch_bounds__(256) k_smem_flat(DIndex ix, DOpts o, Caps cp, 
     uint16_t *Lend = reinterpret_cast<uint16_t *>(lds_raw + (size_t)2 * T * lcap * sizeof(X)) + t;
     FM<X> fm;
     fm.occ = ix.occ;
+    fm.occ32 = ix.occ32;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
     fm.kt = nullptr;
@@ -715,6 +766,7 @@ __global__ void k_kmer_level(DIndex ix, uint4 *tab, int L)
     if (P >= n) return;
     FM<uint32_t> fm;
     fm.occ = ix.occ;
+    fm.occ32 = ix.occ32;
     fm.kt = nullptr;
     fm.K = 0;
     fm.l2_0 = (uint32_t)ix.L2[0]; fm.l2_1 = (uint32_t)ix.L2[1]; fm.l2_2 = (uint32_t)ix.L2[2];
