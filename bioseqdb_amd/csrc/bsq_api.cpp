@@ -49,7 +49,7 @@ hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, cons
 hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
-                           Intv *, int32_t *, uint32_t *, Counters *, int);
+                           Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int);
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
@@ -334,6 +334,7 @@ struct Workspace {
     int64_t zslab_bytes = 0;
     int zslab_blocks = 0;
     int32_t *dlist0 = nullptr, *dlist1 = nullptr, *dcount = nullptr;   // reads deferred by the group kernels
+    uint8_t *lspill = nullptr;   // SMEM list entries beyond the LDS share (main pass), LSPILL per read
     uint32_t *ekey0 = nullptr, *ekey1 = nullptr;   // extension work keys (main pass) and their sort
     int32_t *eidx0 = nullptr, *eidx1 = nullptr;
     void *esort_tmp = nullptr;
@@ -344,7 +345,7 @@ struct Workspace {
         hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
         hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
-        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp);
+        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill);
         *this = Workspace{};
     }
 };
@@ -359,6 +360,8 @@ int64_t scratch_bytes(const Caps &c, int64_t z_cap)
     int64_t m = std::max(std::max(smem, chain), std::max(ext, r2a));
     return (m + 255) & ~255LL;
 }
+
+static const int LSPILL = 48;   // SMEM list entries per read beyond the LDS share
 
 int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64_t z_cap, bool with_sel)
 {
@@ -389,6 +392,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
         HIPCHK(hipMalloc(&w.dcount, 16));
+        HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 2)));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
         HIPCHK(hipMalloc(&w.ekey1, R * 4));
         HIPCHK(hipMalloc(&w.eidx0, R * 4));
@@ -586,15 +590,17 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
-        static const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning experiments
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : ix.seq_len < 0xFFFFFFFFull ? 20 : 16;
+        const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning and the spill test
+        // 15 entries in LDS = 38.4 KB per 256-lane block: 4 blocks (16 waves) per CU; longer lists spill
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : ix.seq_len < 0xFFFFFFFFull ? 15 : 8;
         static const char *alt = getenv("BSQ_SMEM");
         static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
         if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)
             HIPCHK(launch_smem_flat(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                     sblocks));
         else
-            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap));
+            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap,
+                                   w.lspill, tiny_caps() ? 0 : LSPILL));
     } else {
         HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }

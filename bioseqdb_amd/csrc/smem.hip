@@ -171,13 +171,28 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
 // first entry of the k-mer table level for strings of length L: (4^L - 4) / 3
 DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
 
-// LDS list of (x0, x2, end) entries for one lane: entry e at base[e * stride]
+// The lane's list of (x0, x2, end) entries: entries e < cap in LDS (entry e at base[e * stride],
+// lane-interleaved), the next gcap in this read's global spill area (lists longer than the LDS share
+// are rare; they cost global accesses instead of a retry).
 template <typename X>
 struct LList {
     X *x0, *x2;
     uint16_t *end;
     int stride, cap;
-    DEV void set(int e, X a, X b, int en) { x0[e * stride] = a; x2[e * stride] = b; end[e * stride] = (uint16_t)en; }
+    X *gx0, *gx2;
+    uint16_t *gend;
+    int gcap;
+    DEV int total() const { return cap + gcap; }
+    DEV void set(int e, X a, X b, int en)
+    {
+        if (e < cap) { x0[e * stride] = a; x2[e * stride] = b; end[e * stride] = (uint16_t)en; }
+        else { const int g = e - cap; gx0[g] = a; gx2[g] = b; gend[g] = (uint16_t)en; }
+    }
+    DEV void get(int e, X &a, X &b, int &en) const
+    {
+        if (e < cap) { a = x0[e * stride]; b = x2[e * stride]; en = end[e * stride]; }
+        else { const int g = e - cap; a = gx0[g]; b = gx2[g]; en = gend[g]; }
+    }
 };
 
 struct OutSlot {   // the read's output intervals (global), mem grows from the front, mem1 from the back
@@ -211,29 +226,31 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 != ik2) {
-                if (n >= L.cap) { ovf = true; return len; }
+                if (n >= L.total()) { ovf = true; return len; }
                 L.set(n++, ik0, ik2, ikend);
                 if (n2 < (X)min_intv) break;
             }
             ik0 = n0; ik1 = n1; ik2 = n2; ikend = i + 1;
         } else {
-            if (n >= L.cap) { ovf = true; return len; }
+            if (n >= L.total()) { ovf = true; return len; }
             L.set(n++, ik0, ik2, ikend);
             break;
         }
     }
     if (i == len) {
-        if (n >= L.cap) { ovf = true; return len; }
+        if (n >= L.total()) { ovf = true; return len; }
         L.set(n++, ik0, ik2, ikend);
     }
     for (int j = 0; j < (n >> 1); ++j) {   // reverse: longest match first
-        const int a = j * L.stride, b = (n - 1 - j) * L.stride;
-        X t0 = L.x0[a], t2 = L.x2[a];
-        uint16_t te = L.end[a];
-        L.x0[a] = L.x0[b]; L.x2[a] = L.x2[b]; L.end[a] = L.end[b];
-        L.x0[b] = t0; L.x2[b] = t2; L.end[b] = te;
+        X a0, a2, b0, b2;
+        int ae, be;
+        L.get(j, a0, a2, ae);
+        L.get(n - 1 - j, b0, b2, be);
+        L.set(j, b0, b2, be);
+        L.set(n - 1 - j, a0, a2, ae);
     }
-    const int ret = L.end[0];
+    int ret;
+    { X d0, d2; L.get(0, d0, d2, ret); }
     int last_start = 0x7fffffff;
     const int K = fm.K;
     uint32_t wcode = 0;   // q[i .. i+K) packed, first base most significant (positions past the read: 0)
@@ -247,11 +264,10 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
             // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
             // Compaction writes go to nc <= j, below both entries already read.
             const bool hb = j + 1 < n;
-            const X pa0 = L.x0[j * L.stride], pa2 = L.x2[j * L.stride];
-            const int pae = L.end[j * L.stride];
-            const int jb = hb ? j + 1 : j;
-            const X pb0 = L.x0[jb * L.stride], pb2 = L.x2[jb * L.stride];
-            const int pbe = L.end[jb * L.stride];
+            X pa0, pa2, pb0, pb2;
+            int pae, pbe;
+            L.get(j, pa0, pa2, pae);
+            L.get(hb ? j + 1 : j, pb0, pb2, pbe);
             X oa0 = 0, oa2 = 0, ob0 = 0, ob2 = 0;
             if (c >= 0) {
                 // strings q[i .. end) of at most K bases come from the k-mer table
@@ -333,7 +349,7 @@ DEV void wave_add2(unsigned long long *dst, unsigned long long v)
 template <typename X>
 __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
-                                                  Counters *ctr, int lcap)
+                                                  Counters *ctr, int lcap, uint8_t *spill, int gcap)
 {
     extern __shared__ uint8_t lds_raw[];
     const int T = blockDim.x, t = threadIdx.x;
@@ -343,6 +359,13 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     L.end = reinterpret_cast<uint16_t *>(lds_raw + (size_t)2 * T * lcap * sizeof(X)) + t;
     L.stride = T;
     L.cap = lcap;
+    {   // spill area: [x0: n*gcap X][x2: n*gcap X][end: n*gcap u16], this read's gcap entries of each
+        const size_t me = (size_t)(blockIdx.x * T + t) * (size_t)gcap, tot = (size_t)n * (size_t)gcap;
+        L.gx0 = reinterpret_cast<X *>(spill) + me;
+        L.gx2 = reinterpret_cast<X *>(spill) + tot + me;
+        L.gend = reinterpret_cast<uint16_t *>(spill + 2 * tot * sizeof(X)) + me;
+        L.gcap = spill ? gcap : 0;
+    }
     FM<X> fm;
     fm.occ = ix.occ;
     fm.occ32 = ix.occ32;
@@ -427,7 +450,7 @@ static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap *
 
 hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                            const int64_t *offs, int n, Intv *intv, int32_t *n_intv, uint32_t *status, Counters *ctr,
-                           int lcap)
+                           int lcap, uint8_t *spill, int gcap)
 {
     const int T = 256;
     const int grid = (n + T - 1) / T;
@@ -435,11 +458,11 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     if (ix.seq_len < 0xFFFFFFFFull) {
         size_t sh = lds_bytes<uint32_t>(T, lcap);
         hipLaunchKernelGGL(k_smem_lds<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap);
+                           status, ctr, lcap, spill, gcap);
     } else {
         size_t sh = lds_bytes<uint64_t>(T, lcap);
         hipLaunchKernelGGL(k_smem_lds<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap);
+                           status, ctr, lcap, spill, gcap);
     }
     return hipGetLastError();
 }
