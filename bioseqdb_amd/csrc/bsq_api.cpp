@@ -240,7 +240,8 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
     v.kmer = nullptr;
     v.kmer_k = 0;
     v.occ32 = nullptr;
-    if (h.seq_len > 0 && h.seq_len < 0xFFFFFFFFull) {
+    v.wide = h.sa32.empty() ? 1 : 0;
+    if (h.seq_len > 0 && !v.wide) {
         // 64-base blocks: half 0 of each 128-base block keeps its counts, half 1 adds the first 64 bases
         std::vector<OccBlock32> o32(h.occ.size() * 2);
         for (size_t b = 0; b < h.occ.size(); ++b) {
@@ -261,7 +262,7 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
     }
     // k-mer interval table (u32 rows): depth ~log4(rows), at most 11 (89 MB, stays in the Infinity
     // Cache beside the occ array at 100 Mbp); BSQ_KMER_K overrides, 0 disables
-    if (h.seq_len > 0 && h.seq_len < 0xFFFFFFFFull) {
+    if (h.seq_len > 0 && !v.wide) {
         int K = 0;
         while (K < 11 && (1ull << (2 * (K + 1))) <= h.seq_len) ++K;
         if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
@@ -592,7 +593,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning and the spill test
         // 15 entries in LDS = 38.4 KB per 256-lane block: 4 blocks (16 waves) per CU; longer lists spill
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : ix.seq_len < 0xFFFFFFFFull ? 15 : 8;
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 8;
         static const char *alt = getenv("BSQ_SMEM");
         static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
         if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)

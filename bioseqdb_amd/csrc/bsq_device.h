@@ -42,6 +42,8 @@ struct DIndex {
     // (4^|S| - 4)/3 + code(S), code = base-4 value of S with the first base most significant
     const uint32_t *kmer;
     const OccBlock32 *occ32;  // 64-base rank blocks (u32 rows only; nullptr otherwise)
+    int32_t wide;             // 1: 64-bit rows (seq_len >= 2^32, or forced by BSQ_FORCE_WIDE)
+    int32_t pad2;
 };
 
 // mem_opt_t fields the path reads (mem_opt_init defaults + bioseqdb overrides).

@@ -10,6 +10,7 @@
 // The suffix sort is a parallel MSD bucket sort on 8-base prefixes, then per-bucket sorts on the
 // next 32 bases with an exact tie-breaking comparison.
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <atomic>
 #include <cstring>
@@ -178,7 +179,10 @@ int HostIndex::build(int threads, std::string &err)
         }
         bstart[NB] = acc;
     }
-    const bool wide = n >= 0xFFFFFFFFull;
+    // 64-bit rows for texts of >= 2^32 rows; BSQ_FORCE_WIDE=1 selects them for any size (tests of the
+    // 3 Gbp code path on small references)
+    const char *fw = getenv("BSQ_FORCE_WIDE");
+    const bool wide = n >= 0xFFFFFFFFull || (fw && *fw && *fw != '0');
     std::vector<uint64_t> idx64;
     std::vector<uint32_t> idx32;
     if (wide) idx64.resize(n); else idx32.resize(n);

@@ -455,7 +455,7 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int T = 256;
     const int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
-    if (ix.seq_len < 0xFFFFFFFFull) {
+    if (!ix.wide) {
         size_t sh = lds_bytes<uint32_t>(T, lcap);
         hipLaunchKernelGGL(k_smem_lds<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
                            status, ctr, lcap, spill, gcap);
@@ -754,7 +754,7 @@ hipError_t launch_smem_flat(hipStream_t st, const DIndex &ix, const DOpts &o, co
             max_blocks = cus * per;
         if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
     };
-    if (ix.seq_len < 0xFFFFFFFFull) {
+    if (!ix.wide) {
         size_t sh = lds_bytes<uint32_t>(T, lcap);
         clamp(reinterpret_cast<const void *>(k_smem_flat<uint32_t>), sh);
         hipLaunchKernelGGL(k_smem_flat<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,

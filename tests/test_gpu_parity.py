@@ -119,3 +119,15 @@ def test_parity_smem_list_spill(monkeypatch):
     rows, bad = compare(pi, oi, _texts(reads), first_call=7)
     assert rows > 1300
     assert not bad, bad[:20]
+
+
+def test_parity_wide_rows(monkeypatch):
+    """The 64-bit-row code path of the 3 Gbp configs (u64 SA, 128-base occ blocks, no k-mer table, u64
+    SMEM lists with global spill), forced on a small reference."""
+    monkeypatch.setenv("BSQ_FORCE_WIDE", "1")
+    ref = synth.make_reference(1_000_000, n_rows=3, n_run_every=300_000, n_run_len=400)
+    reads = synth.make_reads(ref, 3000, seed=31)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=99)
+    assert rows > 2500
+    assert not bad, bad[:20]
