@@ -90,6 +90,10 @@ SIGNATURES = {
     "bsq_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "bsq_batch_stage_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "bsq_batch_stage_work": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    "bsq_batch_seed": (ctypes.c_int, [_P, _P]),
+    "bsq_batch_intervals": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(ctypes.c_int64)),
+                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                           ctypes.POINTER(ctypes.c_int64)]),
     "bsq_batch_retried": (ctypes.c_int64, [_P]),
 }
 

@@ -1386,6 +1386,43 @@ __global__ void k_collect_overflow(int n, const uint32_t *status, int32_t *list,
 // ------------------------------------------------------------------------------------------------
 namespace bsq {
 
+// seeding-only output (bsq_batch_intervals): per-read interval counts (0 for reads left to the retry pass)
+// and compaction of the main-pass interval slots into one array
+__global__ void k_intv_counts(int n, const int32_t *__restrict__ n_intv, const uint32_t *__restrict__ status,
+                              int64_t *__restrict__ cnt)
+{
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li < n) cnt[li] = status[li] ? 0 : n_intv[li];
+    if (li == n) cnt[n] = 0;
+}
+
+__global__ void k_intv_pack(int n, int cap, const Intv *__restrict__ slots, const int32_t *__restrict__ n_intv,
+                            const uint32_t *__restrict__ status, const int64_t *__restrict__ off,
+                            uint64_t *__restrict__ out)
+{
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n || status[li]) return;
+    const Intv *a = slots + (size_t)li * cap;
+    uint64_t *d = out + 4 * (size_t)off[li];
+    for (int k = 0; k < n_intv[li]; ++k) {
+        d[4 * k + 0] = a[k].x[0]; d[4 * k + 1] = a[k].x[1]; d[4 * k + 2] = a[k].x[2]; d[4 * k + 3] = a[k].info;
+    }
+}
+
+hipError_t launch_intv_counts(hipStream_t st, int n, const int32_t *n_intv, const uint32_t *status, int64_t *cnt)
+{
+    hipLaunchKernelGGL(k_intv_counts, dim3((n + 1 + 255) / 256), dim3(256), 0, st, n, n_intv, status, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_intv_pack(hipStream_t st, int n, int cap, const Intv *slots, const int32_t *n_intv,
+                            const uint32_t *status, const int64_t *off, uint64_t *out)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_intv_pack, dim3((n + 255) / 256), dim3(256), 0, st, n, cap, slots, n_intv, status, off, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_smem(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                        const int64_t *offs, const int32_t *sel, int n, Intv *intv, int32_t *n_intv, uint32_t *status,
                        uint8_t *scratch, Counters *ctr)

@@ -53,6 +53,9 @@ hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Cap
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
+hipError_t launch_intv_counts(hipStream_t, int, const int32_t *, const uint32_t *, int64_t *);
+hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *, const uint32_t *, const int64_t *,
+                            uint64_t *);
 }  // namespace bsq
 
 using namespace bsq;
@@ -450,6 +453,16 @@ struct bsq_batch {
     int64_t *h_pinned_off = nullptr;
     int64_t h_cap = 0, h_cig_cap = 0, h_off_cap = 0;
     int64_t n_hits_main = 0, n_cig_main = 0;   // main-pass results left in the pinned buffers
+    // seeding-only runs (bsq_batch_seed): main-pass intervals stay in the workspace slots, reads that
+    // needed the retry kernel keep theirs here; bsq_batch_intervals packs both on demand
+    int32_t chunk = 0;   // reads per workspace pass; larger batches run in chunks [lo, lo + chunk)
+    int32_t lo = 0;      // first read of the chunk being run (stage kernels see offs + lo, ids + lo)
+    bool seeded = false, seed_packed = false;
+    std::vector<std::pair<int32_t, std::vector<uint64_t>>> seed_retry;
+    std::vector<int64_t> seed_off;
+    std::vector<uint64_t> seed_intv;
+    uint64_t *d_intv = nullptr;
+    int64_t d_intv_cap = 0;
     // results
     std::vector<bsq_hit> res_hits;
     std::vector<uint32_t> res_cig;
@@ -510,6 +523,11 @@ extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_b
     b->device = idx->h.dev->device;
     b->max_reads = max_reads;
     b->max_bases = max_bases;
+    {   // workspace pass size (BSQ_CHUNK overrides; tests use it to exercise multi-chunk batches)
+        const char *e = getenv("BSQ_CHUNK");
+        const int c = e && atoi(e) > 0 ? atoi(e) : (1 << 20);
+        b->chunk = std::max(1, std::min(std::max(max_reads, 1), c));
+    }
     *out = b;
     HIPCHK(hipSetDevice(b->device));
     HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
@@ -543,7 +561,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->codes); hipFree(b->offs); hipFree(b->ids); hipFree(b->ctr);
     hipFree(b->cnt_hits); hipFree(b->cnt_cig); hipFree(b->off_hits); hipFree(b->off_cig); hipFree(b->unresolved);
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
-    hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off);
+    hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off); hipFree(b->d_intv);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
     delete b;
@@ -575,7 +593,7 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
     // (re)allocate the main workspace for this read length
     if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1)) {
         b->main.release();
-        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->max_reads, device_workers(b->device), 32 * 1024, false);
+        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device), 32 * 1024, false);
         if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(b->stream));
@@ -583,12 +601,12 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
 }
 
 // Runs smem -> chain -> extend -> reg2aln on workspace w for n local reads.
-static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const int32_t *sel, bool timed)
+// Seeding (mem_collect_intv) on workspace w: the main-pass LDS kernel, or the large-capacity kernel for
+// the retry pass (sel != nullptr).
+static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const int32_t *sel)
 {
     const DIndex &ix = b->idx->h.dev->view;
     hipStream_t st = b->stream;
-    HIPCHK(hipMemsetAsync(w.status, 0, (size_t)std::max(n, 1) * 4, st));
-    if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning and the spill test
@@ -597,28 +615,38 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         static const char *alt = getenv("BSQ_SMEM");
         static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
         if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)
-            HIPCHK(launch_smem_flat(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap,
+            HIPCHK(launch_smem_flat(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                     sblocks));
         else
-            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, b->offs, n, w.intv, w.n_intv, w.status, b->ctr, lcap,
+            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                    w.lspill, tiny_caps() ? 0 : LSPILL));
     } else {
-        HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
+        HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }
+    return BSQ_OK;
+}
+
+static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const int32_t *sel, bool timed)
+{
+    const DIndex &ix = b->idx->h.dev->view;
+    hipStream_t st = b->stream;
+    HIPCHK(hipMemsetAsync(w.status, 0, (size_t)std::max(n, 1) * 4, st));
+    if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
+    { const int rc = seed_stage(b, w, o, n, sel); if (rc) return rc; }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
-    HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, b->offs, sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
+    HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
                         w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
     const int32_t *order = nullptr;
     static const bool no_sort = getenv("BSQ_EXT_SORT") && getenv("BSQ_EXT_SORT")[0] == '0';
     if (!sel && w.ekey0 && n > 0 && !no_sort) {
         // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
-        HIPCHK(launch_ext_key(st, w.cp, b->offs, sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
+        HIPCHK(launch_ext_key(st, w.cp, (b->offs + b->lo), sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
         size_t tb = w.esort_bytes;
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 16, st));
         order = w.eidx1;
     }
-    HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, b->ids, n, w.chains, w.seeds, w.n_chains, w.regs,
+    HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,
                          w.n_regs, w.status, w.scratch, b->ctr, order));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
     if (!sel && w.cp.max_len <= 1024) {
@@ -631,16 +659,16 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         static const bool no_rsort = getenv("BSQ_R2A_SORT") && getenv("BSQ_R2A_SORT")[0] == '0';
         if (w.ekey0 && !no_rsort) {
             // group balance: reads in order of their band class (the extension's sort buffers are free now)
-            HIPCHK(launch_r2a_key(st, o, w.cp, b->offs, n, w.regs, w.n_regs, w.status, w.ekey0, w.eidx0, w.dcount + 2));
+            HIPCHK(launch_r2a_key(st, o, w.cp, (b->offs + b->lo), n, w.regs, w.n_regs, w.status, w.ekey0, w.eidx0, w.dcount + 2));
             size_t tb = w.esort_bytes;
             HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 3, st));
             r_order = w.eidx1;
         }
-        HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, b->offs, n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
+        HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
                                     w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
                                     w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr));
     } else {
-        HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, b->offs, sel, n, w.regs, w.n_regs, w.hits, w.cigars,
+        HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.regs, w.n_regs, w.hits, w.cigars,
                               w.n_cig, w.status, w.scratch, b->ctr));
     }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_PACK], st));
@@ -711,6 +739,95 @@ static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vect
     return BSQ_OK;
 }
 
+// One workspace pass over reads [b->lo, b->lo + n): main pass, overflow retry, packing.  Results are left
+// in the pinned buffers (zero_copy) or in b->res_* (read_index / read_off local to the chunk).
+static int run_chunk(bsq_batch *b, const DOpts &o, int n, bool &zero_copy)
+{
+    hipStream_t st = b->stream;
+    b->retried = 0;
+    int rc = run_stages(b, b->main, o, n, nullptr, true);
+    if (rc) return rc;
+    // overflowing reads -> retry workspace with large capacities
+    HIPCHK(hipMemsetAsync(b->ovf_count, 0, 4, st));
+    HIPCHK(launch_collect_overflow(st, n, b->main.status, b->ovf_list, b->ovf_count));
+    int32_t novf = 0;
+    HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true, /*copy=*/false);
+    if (rc) return rc;
+    zero_copy = novf == 0;
+    if (novf > 0) {
+        // the retry pass reuses the pinned buffers: keep the main results first
+        b->res_off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
+        b->res_hits.assign(b->h_pinned, b->h_pinned + b->n_hits_main);
+        b->res_cig.assign(b->h_pinned_cig, b->h_pinned_cig + b->n_cig_main);
+        b->retried = novf;
+        std::vector<int32_t> list((size_t)novf);
+        HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
+        std::sort(list.begin(), list.end());
+        const int CH = 256;
+        if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
+            b->retry.release();
+            rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
+            if (rc) return rc;
+        }
+        // per-read replacement results
+        std::vector<std::vector<bsq_hit>> rh((size_t)novf);
+        std::vector<std::vector<uint32_t>> rcg((size_t)novf);
+        for (int s = 0; s < novf; s += CH) {
+            int m = std::min(CH, novf - s);
+            HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
+            rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
+            if (rc) return rc;
+            std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
+            rc = pack_to_host(b, b->retry, m, false, hh, cc, oo, false);
+            if (rc) return rc;
+            for (int j = 0; j < m; ++j) {
+                auto &dst = rh[(size_t)(s + j)];
+                auto &dc = rcg[(size_t)(s + j)];
+                for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
+                    bsq_hit x = hh[(size_t)k];
+                    uint32_t base = (uint32_t)dc.size();
+                    dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
+                    x.cigar_off = base;
+                    dst.push_back(x);
+                }
+            }
+        }
+        // merge into read order
+        std::vector<bsq_hit> mh; std::vector<uint32_t> mc; std::vector<int64_t> mo((size_t)n + 1, 0);
+        size_t li = 0;
+        for (int r = 0; r < n; ++r) {
+            mo[r] = (int64_t)mh.size();
+            if (li < list.size() && list[li] == r) {
+                for (auto x : rh[li]) {
+                    uint32_t base = (uint32_t)mc.size();
+                    mc.insert(mc.end(), rcg[li].begin() + x.cigar_off, rcg[li].begin() + x.cigar_off + x.n_cigar);
+                    x.cigar_off = base; x.read_index = r;
+                    mh.push_back(x);
+                }
+                ++li;
+            } else {
+                for (int64_t k = b->res_off[r]; k < b->res_off[r + 1]; ++k) {
+                    bsq_hit x = b->res_hits[(size_t)k];
+                    uint32_t base = (uint32_t)mc.size();
+                    mc.insert(mc.end(), b->res_cig.begin() + x.cigar_off, b->res_cig.begin() + x.cigar_off + x.n_cigar);
+                    x.cigar_off = base;
+                    mh.push_back(x);
+                }
+            }
+        }
+        mo[n] = (int64_t)mh.size();
+        b->res_hits.swap(mh); b->res_cig.swap(mc); b->res_off.swap(mo);
+    }
+    for (int s = 0; s < STG_N; ++s) {   // per-chunk device time, summed over chunks
+        float ms = 0;
+        hipEventElapsedTime(&ms, b->ev[s], b->ev[s + 1]);
+        b->stage_ms[s] += ms;
+    }
+    return BSQ_OK;
+}
+
 extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq)
 {
     if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
@@ -734,88 +851,47 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     b->res_hits.clear(); b->res_cig.clear(); b->res_off.assign((size_t)n + 1, 0);
     int rc = BSQ_OK;
     bool zero_copy = false;
+    for (int s = 0; s < STG_N; ++s) b->stage_ms[s] = 0;
     if (n > 0 && b->idx->h.seq_len > 0) {
-        rc = run_stages(b, b->main, o, n, nullptr, true);
-        if (rc) return rc;
-        // overflowing reads -> retry workspace with large capacities
-        HIPCHK(hipMemsetAsync(b->ovf_count, 0, 4, st));
-        HIPCHK(launch_collect_overflow(st, n, b->main.status, b->ovf_list, b->ovf_count));
-        int32_t novf = 0;
-        HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true, /*copy=*/false);
-        if (rc) return rc;
-        zero_copy = novf == 0;
-        if (novf > 0) {
-            // the retry pass reuses the pinned buffers: keep the main results first
-            b->res_off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
-            b->res_hits.assign(b->h_pinned, b->h_pinned + b->n_hits_main);
-            b->res_cig.assign(b->h_pinned_cig, b->h_pinned_cig + b->n_cig_main);
-            b->retried = novf;
-            std::vector<int32_t> list((size_t)novf);
-            HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
-            std::sort(list.begin(), list.end());
-            const int CH = 256;
-            if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
-                b->retry.release();
-                rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
+        if (n <= b->chunk) {
+            b->lo = 0;
+            rc = run_chunk(b, o, n, zero_copy);
+            if (rc) return rc;
+        } else {   // chunks of the workspace size, results appended in read order
+            std::vector<bsq_hit> H;
+            std::vector<uint32_t> G;
+            std::vector<int64_t> F((size_t)n + 1, 0);
+            int64_t retried = 0;
+            for (int lo = 0; lo < n; lo += b->chunk) {
+                const int m = std::min(b->chunk, n - lo);
+                bool zc = false;
+                b->lo = lo;
+                rc = run_chunk(b, o, m, zc);
+                b->lo = 0;
                 if (rc) return rc;
-            }
-            // per-read replacement results
-            std::vector<std::vector<bsq_hit>> rh((size_t)novf);
-            std::vector<std::vector<uint32_t>> rcg((size_t)novf);
-            for (int s = 0; s < novf; s += CH) {
-                int m = std::min(CH, novf - s);
-                HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
-                rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
-                if (rc) return rc;
-                std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
-                rc = pack_to_host(b, b->retry, m, false, hh, cc, oo, false);
-                if (rc) return rc;
-                for (int j = 0; j < m; ++j) {
-                    auto &dst = rh[(size_t)(s + j)];
-                    auto &dc = rcg[(size_t)(s + j)];
-                    for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
-                        bsq_hit x = hh[(size_t)k];
-                        uint32_t base = (uint32_t)dc.size();
-                        dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
-                        x.cigar_off = base;
-                        dst.push_back(x);
-                    }
+                retried += b->retried;
+                const bsq_hit *hp = zc ? b->h_pinned : b->res_hits.data();
+                const uint32_t *cp = zc ? b->h_pinned_cig : b->res_cig.data();
+                const int64_t *op = zc ? b->h_pinned_off : b->res_off.data();
+                const int64_t nh = zc ? b->n_hits_main : (int64_t)b->res_hits.size();
+                const int64_t nc = zc ? b->n_cig_main : (int64_t)b->res_cig.size();
+                const int64_t hbase = (int64_t)H.size();
+                const uint32_t cbase = (uint32_t)G.size();
+                for (int r = 0; r < m; ++r) F[(size_t)lo + r] = hbase + op[r];
+                for (int64_t k = 0; k < nh; ++k) {
+                    bsq_hit x = hp[k];
+                    x.read_index += lo;
+                    x.cigar_off += cbase;
+                    H.push_back(x);
                 }
+                G.insert(G.end(), cp, cp + nc);
             }
-            // merge into read order
-            std::vector<bsq_hit> mh; std::vector<uint32_t> mc; std::vector<int64_t> mo((size_t)n + 1, 0);
-            size_t li = 0;
-            for (int r = 0; r < n; ++r) {
-                mo[r] = (int64_t)mh.size();
-                if (li < list.size() && list[li] == r) {
-                    for (auto x : rh[li]) {
-                        uint32_t base = (uint32_t)mc.size();
-                        mc.insert(mc.end(), rcg[li].begin() + x.cigar_off, rcg[li].begin() + x.cigar_off + x.n_cigar);
-                        x.cigar_off = base; x.read_index = r;
-                        mh.push_back(x);
-                    }
-                    ++li;
-                } else {
-                    for (int64_t k = b->res_off[r]; k < b->res_off[r + 1]; ++k) {
-                        bsq_hit x = b->res_hits[(size_t)k];
-                        uint32_t base = (uint32_t)mc.size();
-                        mc.insert(mc.end(), b->res_cig.begin() + x.cigar_off, b->res_cig.begin() + x.cigar_off + x.n_cigar);
-                        x.cigar_off = base;
-                        mh.push_back(x);
-                    }
-                }
-            }
-            mo[n] = (int64_t)mh.size();
-            b->res_hits.swap(mh); b->res_cig.swap(mc); b->res_off.swap(mo);
+            F[(size_t)n] = (int64_t)H.size();
+            b->res_hits.swap(H); b->res_cig.swap(G); b->res_off.swap(F);
+            b->retried = retried;
+            zero_copy = false;
         }
-        // stage timings + algorithmic bytes
-        for (int s = 0; s < STG_N; ++s) {
-            float ms = 0;
-            hipEventElapsedTime(&ms, b->ev[s], b->ev[s + 1]);
-            b->stage_ms[s] = ms;
-        }
+        // algorithmic bytes (stage times were summed over the chunks)
         Counters c[STG_N];
         HIPCHK(hipMemcpy(c, b->ctr, sizeof c, hipMemcpyDeviceToHost));
         b->stage_bytes[STG_SMEM] =
@@ -845,6 +921,165 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->view.n_cigar = (int64_t)b->res_cig.size();
         b->view.cigar = b->res_cig.data();
     }
+    return BSQ_OK;
+}
+
+// ================================================================================================
+// Seeding only (BASELINE.json configs[1]): libbwa mem_collect_intv for every read of the batch
+// ================================================================================================
+// Seeding pass over reads [b->lo, b->lo + n) of the main workspace; reads that overflow get the large-capacity
+// kernel and keep their intervals in b->seed_retry (read index local to the chunk).
+static int seed_chunk(bsq_batch *b, const DOpts &o, int n)
+{
+    hipStream_t st = b->stream;
+    Workspace &w = b->main;
+    b->seed_retry.clear();
+    HIPCHK(hipMemsetAsync(w.status, 0, (size_t)n * 4, st));
+    HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
+    { const int rc = seed_stage(b, w, o, n, nullptr); if (rc) return rc; }
+    HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
+    HIPCHK(hipMemsetAsync(b->ovf_count, 0, 4, st));
+    HIPCHK(launch_collect_overflow(st, n, w.status, b->ovf_list, b->ovf_count));
+    int32_t novf = 0;
+    HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (novf > 0) {   // large-capacity seeding for the reads whose lists or slots overflowed
+        b->retried += novf;
+        std::vector<int32_t> list((size_t)novf);
+        HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
+        std::sort(list.begin(), list.end());
+        const int CH = 256;
+        if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
+            b->retry.release();
+            const int rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
+            if (rc) return rc;
+        }
+        Workspace &r = b->retry;
+        std::vector<int32_t> cnt(CH);
+        std::vector<uint32_t> stt(CH);
+        std::vector<Intv> slots((size_t)CH * r.cp.intv);
+        for (int s0 = 0; s0 < novf; s0 += CH) {
+            const int m = std::min(CH, novf - s0);
+            HIPCHK(hipMemcpyAsync(r.sel, list.data() + s0, (size_t)m * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemsetAsync(r.status, 0, (size_t)m * 4, st));
+            { const int rc = seed_stage(b, r, o, m, r.sel); if (rc) return rc; }
+            HIPCHK(hipMemcpyAsync(cnt.data(), r.n_intv, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(stt.data(), r.status, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(slots.data(), r.intv, (size_t)m * r.cp.intv * sizeof(Intv), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (int j = 0; j < m; ++j) {
+                if (stt[j]) { set_err("read %d exceeded even the retry seeding capacities", b->lo + list[s0 + j]); return BSQ_E_UNSUPPORTED; }
+                std::vector<uint64_t> v((size_t)cnt[j] * 4);
+                for (int k = 0; k < cnt[j]; ++k) {
+                    const Intv &x = slots[(size_t)j * r.cp.intv + k];
+                    v[4 * k] = x.x[0]; v[4 * k + 1] = x.x[1]; v[4 * k + 2] = x.x[2]; v[4 * k + 3] = x.info;
+                }
+                b->seed_retry.emplace_back(list[s0 + j], std::move(v));
+            }
+        }
+    }
+    float ms = 0;
+    hipEventElapsedTime(&ms, b->ev[STG_SMEM], b->ev[STG_CHAIN]);
+    b->stage_ms[STG_SMEM] += ms;
+    return BSQ_OK;
+}
+
+// Appends the intervals of the chunk just seeded (n reads, main slots + b->seed_retry) to seed_off /
+// seed_intv, which hold the previous chunks.
+static int pack_seed_chunk(bsq_batch *b, int n)
+{
+    hipStream_t st = b->stream;
+    Workspace &w = b->main;
+    HIPCHK(launch_intv_counts(st, n, w.n_intv, w.status, b->cnt_hits));
+    size_t tb = b->cub_bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->cub_tmp, tb, b->cnt_hits, b->off_hits, n + 1, st));
+    std::vector<int64_t> off((size_t)n + 1);
+    HIPCHK(hipMemcpyAsync(off.data(), b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int64_t tot = off[n];
+    if (tot > b->d_intv_cap) {
+        hipFree(b->d_intv);
+        b->d_intv_cap = std::max<int64_t>(tot, 1);
+        HIPCHK(hipMalloc(&b->d_intv, (size_t)b->d_intv_cap * 32));
+    }
+    std::vector<uint64_t> packed((size_t)tot * 4);
+    HIPCHK(launch_intv_pack(st, n, w.cp.intv, w.intv, w.n_intv, w.status, b->off_hits, b->d_intv));
+    if (tot) HIPCHK(hipMemcpyAsync(packed.data(), b->d_intv, (size_t)tot * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    size_t ri = 0;
+    for (int li = 0; li < n; ++li) {
+        b->seed_off.push_back((int64_t)(b->seed_intv.size() / 4));
+        if (ri < b->seed_retry.size() && b->seed_retry[ri].first == li) {
+            const auto &v = b->seed_retry[ri++].second;
+            b->seed_intv.insert(b->seed_intv.end(), v.begin(), v.end());
+        } else {
+            b->seed_intv.insert(b->seed_intv.end(), packed.begin() + 4 * off[li], packed.begin() + 4 * off[li + 1]);
+        }
+    }
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
+{
+    if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (opts->max_occ <= 0 || opts->min_seed_len <= 0) { set_err("max_occ and min_seed_len must be positive"); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    const int n = b->n_reads;
+    const DOpts o = make_dopts(*opts);
+    b->seeded = false;
+    b->seed_packed = false;
+    b->seed_retry.clear();
+    b->seed_off.clear();
+    b->seed_intv.clear();
+    b->retried = 0;
+    HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, b->stream));
+    for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
+    if (n > 0 && b->idx->h.seq_len > 0) {
+        if (n <= b->chunk) {   // intervals stay in the workspace until bsq_batch_intervals
+            b->lo = 0;
+            const int rc = seed_chunk(b, o, n);
+            if (rc) return rc;
+        } else {               // the workspace is reused per chunk: pack each chunk's intervals as it finishes
+            for (int lo = 0; lo < n; lo += b->chunk) {
+                const int m = std::min(b->chunk, n - lo);
+                b->lo = lo;
+                int rc = seed_chunk(b, o, m);
+                if (!rc) rc = pack_seed_chunk(b, m);
+                b->lo = 0;
+                if (rc) return rc;
+            }
+            b->seed_off.push_back((int64_t)(b->seed_intv.size() / 4));
+            b->seed_packed = true;
+        }
+        Counters c[STG_N];
+        HIPCHK(hipMemcpy(c, b->ctr, sizeof c, hipMemcpyDeviceToHost));
+        b->stage_bytes[STG_SMEM] =
+            32.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
+        b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
+    }
+    b->seeded = true;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const uint64_t **intv, int64_t *n_intv)
+{
+    if (!b || !read_off || !intv || !n_intv) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (!b->seeded) { set_err("no seeding run on this batch (call bsq_batch_seed)"); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    const int n = b->n_reads;
+    if (!b->seed_packed) {
+        b->seed_off.clear();
+        b->seed_intv.clear();
+        if (n > 0 && b->idx->h.seq_len > 0) {
+            const int rc = pack_seed_chunk(b, n);
+            if (rc) return rc;
+        } else b->seed_off.assign((size_t)n, 0);
+        b->seed_off.push_back((int64_t)(b->seed_intv.size() / 4));
+        b->seed_packed = true;
+    }
+    *read_off = b->seed_off.data();
+    *intv = b->seed_intv.data();
+    *n_intv = b->seed_off[n];
     return BSQ_OK;
 }
 

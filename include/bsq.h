@@ -137,6 +137,16 @@ void bsq_batch_free(bsq_batch *b);
 int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int64_t *offsets, int32_t n_reads);
 /* Run the whole alignment pipeline on the staged reads and copy the packed hits to the host. */
 int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq);
+/* Seeding only (BASELINE.json configs[1]; libbwa mem_collect_intv as called by mem_align1_core,
+ * bwamem.c, for every read): SMEM passes 1 and 2 plus bwt_seed_strategy1, kept if end-start >=
+ * min_seed_len, sorted by info.  The intervals stay on the device until bsq_batch_intervals. */
+int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts);
+/* Intervals of the last bsq_batch_seed in read order: read i owns intervals [read_off[i],
+ * read_off[i+1]); interval k is intv[4k..4k+3] = (x[0], x[1], x[2], info = qbeg<<32 | qend).  x[1]
+ * (the reverse-strand interval start) is not part of the contract (the main-pass kernel does not keep
+ * it for SMEMs; nothing on the alignment path reads it).  Borrowed arrays, valid until the next call
+ * on the batch. */
+int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const uint64_t **intv, int64_t *n_intv);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
 /* Per-stage device time of the last run in ms, measured with HIP events on the batch stream.

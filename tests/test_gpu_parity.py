@@ -131,3 +131,15 @@ def test_parity_wide_rows(monkeypatch):
     rows, bad = compare(pi, oi, _texts(reads), first_call=99)
     assert rows > 2500
     assert not bad, bad[:20]
+
+
+def test_parity_chunked_batch(monkeypatch):
+    """A batch larger than the workspace runs in chunks (reads resident, workspace reused); the
+    retry pass and the read/CIGAR offsets are per chunk, the results must be unchanged."""
+    monkeypatch.setenv("BSQ_CHUNK", "700")
+    ref = synth.make_reference(500_000, n_run_every=200_000, n_run_len=300, dup_frac=0.02)
+    reads = synth.make_reads(ref, 2600, seed=37)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=5)
+    assert rows > 2200
+    assert not bad, bad[:20]
