@@ -2,6 +2,10 @@
 """bench.py -- BASELINE.json metric: aligned reads/s, 150 bp synthetic reads vs a 100 Mbp synthetic
 reference, full BWA-MEM seed + extend + CIGAR (configs[2], "C3"), on N MI355X GPUs.
 
+--config c2 measures configs[1] (FM-index seeding only, mem_collect_intv) and --config c4 configs[3]
+(10M reads vs a 3 Gbp reference of 24 rows x 125 Mbp: 64-bit rows, index > Infinity Cache, the batch
+runs in 1M-read workspace chunks); the default (no flags) is C3.
+
 One step = one pass of the whole alignment path (libbsq: smem -> chain -> extend -> reg2aln -> pack ->
 D2H of the hit records) over one batch of reads already resident in HBM; with N > 1 each rank aligns
 its own batch (weak scaling, read-sharded) and the hit records are gathered to rank 0 over RCCL
@@ -56,6 +60,73 @@ def default_opts(n_refs: int) -> N.Opts:
     return N.Opts(19, max(500, 2 * n_refs), 1, 4, 5, 5, 100, 100, 6, 6, 1, 1)
 
 
+CONFIGS = {
+    "c3": dict(reads=1_000_000, ref_bp=100_000_000, rows=1, seeding=False, metric=METRIC,
+               label="C3: 150 bp reads vs 100 Mbp synthetic reference, full seed + banded SW extension + CIGAR "
+                     "(BASELINE.json configs[2]); bwa_opts() SQL defaults"),
+    "c2": dict(reads=1_000_000, ref_bp=100_000_000, rows=1, seeding=True,
+               metric="seeded reads/sec (150 bp vs 100 Mbp ref, FM-index seeding only) on 1 MI355X",
+               label="C2: 150 bp reads vs 100 Mbp synthetic reference, FM-index seeding only (mem_collect_intv: "
+                     "SMEM passes 1+2 + seed strategy; BASELINE.json configs[1]); intervals left in HBM"),
+    "c4": dict(reads=10_000_000, ref_bp=3_000_000_000, rows=24, seeding=False,
+               metric="aligned reads/sec (150 bp vs 3 Gbp ref) on 1 MI355X; bit-exact vs libbwa",
+               label="C4: 150 bp reads vs a 3 Gbp synthetic reference (24 rows x 125 Mbp; 64-bit rows), full "
+                     "seed + extension + CIGAR (BASELINE.json configs[3]); 1M-read workspace chunks"),
+}
+
+_FNV_P = np.uint64(0x100000001B3)
+
+
+def fnv_vec(h: np.ndarray, v: np.ndarray) -> np.ndarray:
+    v = v.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        for i in range(8):
+            h = (h ^ ((v >> np.uint64(8 * i)) & np.uint64(0xFF))) * _FNV_P
+    return h
+
+
+def gpu_checksum_vec(H, n_reads: int) -> int:
+    """The oracle's orc_align_batch checksum (per-read FNV, summed), vectorised over reads."""
+    off = np.ctypeslib.as_array(H.read_off, shape=(n_reads + 1,)).astype(np.int64)
+    nh = int(off[n_reads] - off[0])
+    hits = np.ctypeslib.as_array(H.hits, shape=(max(nh, 1),))[:nh] if nh else None
+    ncig = int(H.n_cigar)
+    cig = np.ctypeslib.as_array(H.cigar, shape=(max(ncig, 1),)) if ncig else np.zeros(1, np.uint32)
+    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64), np.arange(n_reads, dtype=np.uint64))
+    cnt = off[1:] - off[:-1]
+    for k in range(int(cnt.max()) if n_reads else 0):
+        m = cnt > k
+        x = hits[(off[:-1][m] + k) - off[0]]
+        hm = h[m]
+        for col in (x["rb"].astype(np.int64).view(np.uint64), x["re"].astype(np.int64).view(np.uint64),
+                    x["qb"].astype(np.uint32), x["qe"].astype(np.uint32), x["score"].astype(np.uint32),
+                    np.where(x["is_secondary"] != 0, 0x100, 0).astype(np.uint64)):
+            hm = fnv_vec(hm, col)
+        nc = x["n_cigar"].astype(np.int64)
+        co = x["cigar_off"].astype(np.int64)
+        for c in range(int(nc.max()) if len(nc) else 0):
+            mc = nc > c
+            hm[mc] = fnv_vec(hm[mc], cig[co[mc] + c])
+        h[m] = hm
+    with np.errstate(over="ignore"):
+        return int(h.sum(dtype=np.uint64))
+
+
+def intv_checksum_vec(off: np.ndarray, iv: np.ndarray, n_reads: int) -> int:
+    """The oracle's orc_seed_batch checksum over (x[0], x[2], info), vectorised over reads."""
+    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64), np.arange(n_reads, dtype=np.uint64))
+    cnt = off[1:n_reads + 1] - off[:n_reads]
+    for k in range(int(cnt.max()) if n_reads else 0):
+        m = cnt > k
+        row = iv[off[:n_reads][m] + k]
+        hm = h[m]
+        for col in (row[:, 0], row[:, 2], row[:, 3]):
+            hm = fnv_vec(hm, col)
+        h[m] = hm
+    with np.errstate(over="ignore"):
+        return int(h.sum(dtype=np.uint64))
+
+
 def fnv(h: int, v: int) -> int:
     for i in range(8):
         h ^= (v >> (8 * i)) & 0xFF
@@ -85,15 +156,21 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU per step")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="c3 (default, the BASELINE metric), c2 (seeding only), c4 (3 Gbp reference)")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU per step (default: the config's)")
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--ref-bp", type=int, default=100_000_000)
+    ap.add_argument("--ref-bp", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.reads = args.reads or cfg["reads"]
+    args.ref_bp = args.ref_bp or cfg["ref_bp"]
+    default_shape = args.reads == cfg["reads"] and args.ref_bp == cfg["ref_bp"]
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,7 +192,7 @@ def main() -> int:
             dist.init_process_group("gloo")
     L = N.lib()
     t0 = time.time()
-    ref = synth.make_reference(args.ref_bp)
+    ref = synth.make_reference(args.ref_bp, n_rows=cfg["rows"])
     reads = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + rank)
     t_gen = time.time() - t0
 
@@ -149,6 +226,9 @@ def main() -> int:
         f"seq_len {L.bsq_index_seq_len(idx)}")
 
     def step():
+        if cfg["seeding"]:
+            N.check(L.bsq_batch_seed(batch, ctypes.byref(opts)))
+            return
         N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
         if dist is not None:   # exchange step: hit records + CIGARs of every rank to the caller
             import torch
@@ -195,10 +275,13 @@ def main() -> int:
     stage_bytes /= max(args.steps, 1)
     stage_work /= max(args.steps, 1)
     H = L.bsq_batch_hits(batch).contents
-    n_hits = int(H.n_hits)
+    n_hits = int(H.n_hits) if not cfg["seeding"] else 0
     retried = int(L.bsq_batch_retried(batch))
     names = [L.bsq_stage_name(i).decode() for i in range(6)]
-    kern = {names[i]: float(stage_ms[i]) for i in range(4)}
+    kern = {names[i]: float(stage_ms[i]) for i in range(1 if cfg["seeding"] else 4)}
+    # measured PMC traffic exists for the default C3 shape only (profiles/traffic.json)
+    tr = (lambda stage: traffic_for(stage, args.reads)) if (args.config == "c3" and default_shape) else \
+        (lambda stage: (None, None))
     dom = max(kern, key=kern.get)
     di = names.index(dom)
     achieved = stage_bytes[di] / (stage_ms[di] * 1e-3) / 1e9 if stage_ms[di] > 0 else 0.0
@@ -206,7 +289,7 @@ def main() -> int:
     total_reads = args.reads * world
     value = total_reads * args.steps / elapsed
     result = {
-        "metric": METRIC,
+        "metric": cfg["metric"],
         "value": round(value, 1),
         "unit": "reads/s",
         "n_gpus": world,
@@ -219,26 +302,26 @@ def main() -> int:
         "dtype": "int32",
         "data": "synthetic",
         "config": {
-            "workload": "C3: 150 bp reads vs 100 Mbp synthetic reference, full seed + banded SW extension + CIGAR "
-                        "(BASELINE.json configs[2]); bwa_opts() SQL defaults",
+            "workload": cfg["label"],
             "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
             "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
         },
         "roofline": {
             "bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_for(dom, args.reads)[0],
-            "traffic_source": f"profiles/traffic.json ({traffic_for(dom, args.reads)[1]} PMC FETCH_SIZE+WRITE_SIZE per launch)",
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": tr(dom)[0],
+            "traffic_source": (f"profiles/traffic.json ({tr(dom)[1]} PMC FETCH_SIZE+WRITE_SIZE per launch)"
+                               if tr(dom)[0] else "not measured for this shape"),
             "algorithmic_bytes_per_launch": float(stage_bytes[di]), "launch_ms": round(float(stage_ms[di]), 3),
         },
         "kernels": {
             STAGE_KERNEL[nm]: {
                 "ms": round(float(stage_ms[i]), 3), "algorithmic_bytes": float(stage_bytes[i]),
                 "achieved_gbs": round(stage_bytes[i] / (stage_ms[i] * 1e-3) / 1e9, 2) if stage_ms[i] > 0 else 0.0,
-                "traffic_bytes": traffic_for(nm, args.reads)[0],
+                "traffic_bytes": tr(nm)[0],
                 "work": float(stage_work[i]),
-                "traffic_gbs": (round(traffic_for(nm, args.reads)[0] / (stage_ms[i] * 1e-3) / 1e9, 2)
-                                if traffic_for(nm, args.reads)[0] and stage_ms[i] > 0 else None),
-            } for i, nm in enumerate(names[:4])
+                "traffic_gbs": (round(tr(nm)[0] / (stage_ms[i] * 1e-3) / 1e9, 2)
+                                if tr(nm)[0] and stage_ms[i] > 0 else None),
+            } for i, nm in enumerate(names[:1 if cfg["seeding"] else 4])
         },
         "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
         "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
@@ -263,8 +346,12 @@ def main() -> int:
         def run_cpu(n, th):
             ck = ctypes.c_uint64()
             t = time.perf_counter()
-            nreg = O.lib().orc_align_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, 0, th,
-                                           ctypes.byref(ck))
+            if cfg["seeding"]:
+                nreg = O.lib().orc_seed_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, th,
+                                              ctypes.byref(ck))
+            else:
+                nreg = O.lib().orc_align_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, 0, th,
+                                               ctypes.byref(ck))
             return time.perf_counter() - t, nreg, ck.value
 
         dt, _, _ = run_cpu(min(2000, reads.n), threads)            # calibration / warm-up
@@ -272,14 +359,24 @@ def main() -> int:
         sample = int(min(reads.n, max(2000, rate * args.cpu_seconds)))
         dt, nreg, ck = run_cpu(sample, threads)
         dt1, _, _ = run_cpu(min(500, reads.n), 1)
-        gck = gpu_checksum(H, sample)
+        if cfg["seeding"]:
+            ro = ctypes.POINTER(ctypes.c_int64)()
+            ivp = ctypes.POINTER(ctypes.c_uint64)()
+            nt = ctypes.c_int64()
+            N.check(L.bsq_batch_intervals(batch, ctypes.byref(ro), ctypes.byref(ivp), ctypes.byref(nt)))
+            soff = np.ctypeslib.as_array(ro, shape=(reads.n + 1,))
+            siv = np.ctypeslib.as_array(ivp, shape=(max(int(nt.value), 1) * 4,))[: int(nt.value) * 4].reshape(-1, 4)
+            gck = intv_checksum_vec(soff, siv, sample)
+        else:
+            gck = gpu_checksum_vec(H, sample)
         result["cpu_baseline"] = {
             "value": round(sample / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} reads of the same batch, CPU oracle (oracle/bwa_oracle.c, -O2), "
                       f"{threads} threads; 1-thread rate {round(min(500, reads.n) / dt1, 1)} reads/s on 500 reads",
             "value_1thread": round(min(500, reads.n) / dt1, 1),
         }
-        result["parity_sample"] = {"reads": sample, "regions": int(nreg), "checksum_match": bool(gck == ck)}
+        result["parity_sample"] = {"reads": sample, ("intervals" if cfg["seeding"] else "regions"): int(nreg),
+                                   "checksum_match": bool(gck == ck)}
         result["gpu_vs_cpu"] = round(value / (sample / dt), 1)
     if rank == 0:
         print(json.dumps(result), flush=True)

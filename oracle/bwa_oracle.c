@@ -1712,6 +1712,48 @@ static void *batch_worker(void *arg)
     return NULL;
 }
 
+/* seeding only (bench C2 cpu_baseline): mem_collect_intv per read; checksum over (x[0], x[2], info) */
+static void *seed_worker(void *arg)
+{
+    job_t *j = arg;
+    intv_v mem = {0, 0, 0}, mem1 = {0, 0, 0}, tmpv[2] = {{0, 0, 0}, {0, 0, 0}};
+    uint64_t ck = 0;
+    for (int r = j->lo; r < j->hi; ++r) {
+        int len = (int)(j->off[r + 1] - j->off[r]);
+        mem_collect_intv(j->opt, j->idx, len, j->codes + j->off[r], &mem, &mem1, tmpv);
+        uint64_t h = 0xcbf29ce484222325ULL;
+        h = fnv(h, (uint64_t)r);
+        for (size_t i = 0; i < mem.n; ++i) {
+            h = fnv(h, mem.a[i].x[0]); h = fnv(h, mem.a[i].x[2]); h = fnv(h, mem.a[i].info);
+        }
+        ck += h;
+        j->nreg += (int64_t)mem.n;
+    }
+    j->ck = ck;
+    free(mem.a); free(mem1.a); free(tmpv[0].a); free(tmpv[1].a);
+    return NULL;
+}
+
+int64_t orc_seed_batch(const orc_index *idx, const orc_opts *o, const uint8_t *codes, const int64_t *offsets, int n,
+                       int threads, uint64_t *checksum)
+{
+    mopt_t opt; make_opt(o, &opt);
+    if (!idx->built) { if (checksum) *checksum = 0; return 0; }
+    if (threads < 1) threads = 1;
+    pthread_t *th = malloc(sizeof(pthread_t) * (size_t)threads);
+    job_t *jobs = calloc((size_t)threads, sizeof(job_t));
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (job_t){ idx, &opt, codes, offsets, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads),
+                           0, 0, 0, 0 };
+        pthread_create(&th[t], NULL, seed_worker, &jobs[t]);
+    }
+    int64_t nint = 0; uint64_t ck = 0;
+    for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); nint += jobs[t].nreg; ck += jobs[t].ck; }
+    free(th); free(jobs);
+    if (checksum) *checksum = ck;
+    return nint;
+}
+
 int64_t orc_align_batch(const orc_index *idx, const orc_opts *o, const uint8_t *codes, const int64_t *offsets,
                         int n, uint64_t first_call, int threads, uint64_t *checksum)
 {

@@ -93,6 +93,10 @@ int orc_collect_intv(const orc_index *idx, const orc_opts *opt, const uint8_t *q
 /* Bench helper: aligns n reads (nt4 codes, concatenated, offsets[n+1]) with `threads` POSIX threads,
  * returning the number of regions and a 64-bit FNV checksum of (read, rb, re, qb, qe, score, flag,
  * cigar) in *checksum.  lrand ids: orc_lrand48_at(first_call + i). */
+/* Seeding only over reads [0, n) (bench C2 cpu_baseline): returns the number of intervals; *checksum =
+ * sum over reads of FNV(read, (x[0], x[2], info) of each interval). */
+int64_t orc_seed_batch(const orc_index *idx, const orc_opts *opt, const uint8_t *codes, const int64_t *offsets, int n,
+                       int threads, uint64_t *checksum);
 int64_t orc_align_batch(const orc_index *idx, const orc_opts *opt, const uint8_t *codes, const int64_t *offsets,
                         int n, uint64_t first_call, int threads, uint64_t *checksum);
 

@@ -62,6 +62,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(OrcRegion), ctypes.c_int]),
             "orc_collect_intv": (ctypes.c_int, [P, ctypes.POINTER(OrcOpts), P, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+            "orc_seed_batch": (ctypes.c_int64, [P, ctypes.POINTER(OrcOpts), P, P, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_uint64)]),
             "orc_align_batch": (ctypes.c_int64, [P, ctypes.POINTER(OrcOpts), P, P, ctypes.c_int, ctypes.c_uint64,
                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
             "orc_ksw_extend2": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P] + [ctypes.c_int] * 8 +
