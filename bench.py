@@ -55,6 +55,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class Heartbeat:
+    """A line on stderr every `period` s naming the current phase (long C4 setups stay visibly alive)."""
+
+    def __init__(self, tag: str, period: float = 60.0):
+        import threading
+        self.phase, self.t0, self.tag = "start", time.time(), tag
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, args=(period,), daemon=True)
+        self._th.start()
+
+    def _run(self, period):
+        while not self._stop.wait(period):
+            log(f"[{self.tag}] {self.phase} ... {time.time() - self.t0:.0f}s")
+
+    def stop(self):
+        self._stop.set()
+
+
 def default_opts(n_refs: int) -> N.Opts:
     # effective SQL defaults incl. the bwa_opts() field-order quirk (Q1): e_del=6, o_ins=1
     return N.Opts(19, max(500, 2 * n_refs), 1, 4, 5, 5, 100, 100, 6, 6, 1, 1)
@@ -191,6 +209,8 @@ def main() -> int:
             xdev = torch.device("cpu")
             dist.init_process_group("gloo")
     L = N.lib()
+    hb = Heartbeat(f"bench r{rank}")
+    hb.phase = "generating the reference and reads"
     t0 = time.time()
     ref = synth.make_reference(args.ref_bp, n_rows=cfg["rows"])
     reads = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + rank)
@@ -207,10 +227,12 @@ def main() -> int:
         L.bsq_free(p)
         ref_ns.append(buf)
         N.check(L.bsq_index_add_ref(idx, i + 1, ctypes.addressof(buf)))
+    hb.phase = "building the index on the host"
     t0 = time.time()
     N.check(L.bsq_index_build(idx, 0))
     t_build = time.time() - t0
     t0 = time.time()
+    hb.phase = "uploading the index"
     N.check(L.bsq_index_upload(idx, gpu))
     t_upload = time.time() - t0
     opts = default_opts(len(ref.rows))
@@ -240,6 +262,7 @@ def main() -> int:
             cb = np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc]
             D.gather_records(np.concatenate([hb, cb]), device=xdev)
 
+    hb.phase = "aligning"
     for _ in range(args.warmup):
         step()
     stage_ms = np.zeros(6)
@@ -330,6 +353,7 @@ def main() -> int:
     }
 
     # ---- CPU baseline: the oracle on this host, bounded sample, rank 0 at N = 1 only ----
+    hb.phase = "CPU baseline"
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_py as O
@@ -378,6 +402,7 @@ def main() -> int:
         result["parity_sample"] = {"reads": sample, ("intervals" if cfg["seeding"] else "regions"): int(nreg),
                                    "checksum_match": bool(gck == ck)}
         result["gpu_vs_cpu"] = round(value / (sample / dt), 1)
+    hb.stop()
     if rank == 0:
         print(json.dumps(result), flush=True)
     L.bsq_batch_free(batch)

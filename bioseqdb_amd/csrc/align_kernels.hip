@@ -1340,7 +1340,7 @@ __global__ void k_counts(int n, SlotView mv, SlotView rv, const int32_t *retry_s
 
 __global__ void k_pack(int n, SlotView mv, SlotView rv, const int32_t *retry_slot, const int64_t *off_hits,
                        const int64_t *off_cig, const int64_t *ann_off, const int64_t *ann_id, bsq_hit *out,
-                       uint32_t *out_cig)
+                       uint32_t *out_cig, int read_base, int64_t cig_base)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1361,8 +1361,8 @@ __global__ void k_pack(int n, SlotView mv, SlotView rv, const int32_t *retry_slo
         b.qb = h.qb; b.qe = h.qe; b.score = h.score; b.rid = h.rid;
         b.is_primary = (h.flag & 0x100) == 0; b.is_secondary = (h.flag & 0x100) != 0; b.is_reverse = h.is_rev != 0;
         b.pad0 = 0;
-        b.read_index = i;
-        b.cigar_off = (uint32_t)oc; b.n_cigar = (uint32_t)h.n_cigar;
+        b.read_index = read_base + i;   // batch-wide read and CIGAR-arena positions
+        b.cigar_off = (uint32_t)(cig_base + oc); b.n_cigar = (uint32_t)h.n_cigar;
         const uint32_t *src = v.cigars + ((size_t)slot * v.cp.regs + g) * v.cp.cigar;
         for (int t = 0; t < h.n_cigar; ++t) out_cig[oc + t] = src[t];
         oc += h.n_cigar;
@@ -1516,10 +1516,23 @@ hipError_t launch_counts(hipStream_t st, int n, const SlotView &mv, const SlotVi
 
 hipError_t launch_pack(hipStream_t st, int n, const SlotView &mv, const SlotView &rv, const int32_t *retry_slot,
                        const int64_t *off_hits, const int64_t *off_cig, const int64_t *ann_off, const int64_t *ann_id,
-                       bsq_hit *out, uint32_t *out_cig)
+                       bsq_hit *out, uint32_t *out_cig, int read_base, int64_t cig_base)
 {
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, st, n, mv, rv, retry_slot, off_hits, off_cig, ann_off,
-                       ann_id, out, out_cig);
+                       ann_id, out, out_cig, read_base, cig_base);
+    return hipGetLastError();
+}
+
+__global__ void k_add_base(int64_t *v, int n, int64_t base)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] += base;
+}
+
+hipError_t launch_add_base(hipStream_t st, int64_t *v, int n, int64_t base)
+{
+    if (n <= 0 || base == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_add_base, dim3((n + 255) / 256), dim3(256), 0, st, v, n, base);
     return hipGetLastError();
 }
 

@@ -40,7 +40,8 @@ struct SlotView { const Hit *hits; const uint32_t *cigars; const int32_t *n_regs
 hipError_t launch_counts(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const uint32_t *, int64_t *,
                          int64_t *, unsigned long long *);
 hipError_t launch_pack(hipStream_t, int, const SlotView &, const SlotView &, const int32_t *, const int64_t *,
-                       const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *);
+                       const int64_t *, const int64_t *, const int64_t *, bsq_hit *, uint32_t *, int, int64_t);
+hipError_t launch_add_base(hipStream_t, int64_t *, int, int64_t);
 hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *, int32_t *);
 hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *,
                                 const int64_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *,
@@ -263,15 +264,15 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
         HIPCHK(hipMemcpy(d->occ32, o32.data(), o32.size() * sizeof(OccBlock32), hipMemcpyHostToDevice));
         v.occ32 = d->occ32;
     }
-    // k-mer interval table (u32 rows): depth ~log4(rows), at most 11 (89 MB, stays in the Infinity
-    // Cache beside the occ array at 100 Mbp); BSQ_KMER_K overrides, 0 disables
-    if (h.seq_len > 0 && !v.wide) {
+    // k-mer interval table: depth ~log4(rows), at most 11 (u32 rows: 89 MB, stays in the Infinity Cache
+    // beside the occ array at 100 Mbp; 64-bit rows: 32-B entries, 179 MB); BSQ_KMER_K overrides, 0 disables
+    if (h.seq_len > 0) {
         int K = 0;
         while (K < 11 && (1ull << (2 * (K + 1))) <= h.seq_len) ++K;
         if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
         if (K > 0) {
             const size_t entries = (((size_t)1 << (2 * (K + 1))) - 4) / 3;
-            HIPCHK(hipMalloc(&d->kmer, entries * 16));
+            HIPCHK(hipMalloc(&d->kmer, entries * (v.wide ? 32 : 16)));
             v.kmer = d->kmer;
             HIPCHK(launch_kmer_build(nullptr, v, d->kmer, K));
             HIPCHK(hipDeviceSynchronize());
@@ -452,7 +453,6 @@ struct bsq_batch {
     uint32_t *h_pinned_cig = nullptr;
     int64_t *h_pinned_off = nullptr;
     int64_t h_cap = 0, h_cig_cap = 0, h_off_cap = 0;
-    int64_t n_hits_main = 0, n_cig_main = 0;   // main-pass results left in the pinned buffers
     // seeding-only runs (bsq_batch_seed): main-pass intervals stay in the workspace slots, reads that
     // needed the retry kernel keep theirs here; bsq_batch_intervals packs both on demand
     int32_t chunk = 0;   // reads per workspace pass; larger batches run in chunks [lo, lo + chunk)
@@ -464,6 +464,9 @@ struct bsq_batch {
     uint64_t *d_intv = nullptr;
     int64_t d_intv_cap = 0;
     // results
+    std::vector<bsq_hit> main_hits;  // main-pass results of a chunk that needed the retry pass
+    std::vector<uint32_t> main_cig;
+    std::vector<int64_t> main_off;
     std::vector<bsq_hit> res_hits;
     std::vector<uint32_t> res_cig;
     std::vector<int64_t> res_off;
@@ -676,9 +679,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
 }
 
 // Packs workspace w (n local reads) into host vectors hits/cig/off (hits with read_index = local).
-static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vector<bsq_hit> &hits,
-                        std::vector<uint32_t> &cig, std::vector<int64_t> &off, bool allow_unresolved,
-                        bool copy = true)
+static int pack_device(bsq_batch *b, Workspace &w, int n, bool allow_unresolved, int read_base, int64_t cig_base,
+                       int64_t tot[2])
 {
     hipStream_t st = b->stream;
     SlotView v{w.hits, w.cigars, w.n_regs, w.n_cig, w.cp};
@@ -689,7 +691,6 @@ static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vect
     size_t tb = b->cub_bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->cub_tmp, tb, b->cnt_hits, b->off_hits, n + 1, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->cub_tmp, tb, b->cnt_cig, b->off_cig, n + 1, st));
-    int64_t tot[2];
     unsigned long long unres = 0;
     HIPCHK(hipMemcpyAsync(&tot[0], b->off_hits + n, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&tot[1], b->off_cig + n, 8, hipMemcpyDeviceToHost, st));
@@ -706,45 +707,70 @@ static int pack_to_host(bsq_batch *b, Workspace &w, int n, bool timed, std::vect
         b->out_cig_cap = std::max<int64_t>(tot[1], 2 * b->out_cig_cap);
         HIPCHK(hipMalloc(&b->d_out_cig, (size_t)b->out_cig_cap * 4));
     }
-    if (tot[0] > b->h_cap) {
-        hipHostFree(b->h_pinned);
-        b->h_cap = std::max<int64_t>(tot[0], 2 * b->h_cap);
-        HIPCHK(hipHostMalloc((void **)&b->h_pinned, (size_t)b->h_cap * sizeof(bsq_hit)));
-    }
-    if (tot[1] > b->h_cig_cap) {
-        hipHostFree(b->h_pinned_cig);
-        b->h_cig_cap = std::max<int64_t>(tot[1], 2 * b->h_cig_cap);
-        HIPCHK(hipHostMalloc((void **)&b->h_pinned_cig, (size_t)b->h_cig_cap * 4));
-    }
     const DeviceIndex *d = b->idx->h.dev;
-    if (n && tot[0]) HIPCHK(launch_pack(st, n, v, v, nullptr, b->off_hits, b->off_cig, d->ann_off, d->ann_id, b->d_out, b->d_out_cig));
-    if ((int64_t)n + 1 > b->h_off_cap) {
-        hipHostFree(b->h_pinned_off);
-        b->h_off_cap = std::max<int64_t>((int64_t)n + 1, 2 * b->h_off_cap);
-        HIPCHK(hipHostMalloc((void **)&b->h_pinned_off, (size_t)b->h_off_cap * 8));
-    }
-    if (timed) HIPCHK(hipEventRecord(b->ev[STG_D2H], st));
-    HIPCHK(hipMemcpyAsync(b->h_pinned_off, b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
-    if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
-    if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
-    if (timed) HIPCHK(hipEventRecord(b->ev[STG_N], st));
-    HIPCHK(hipStreamSynchronize(st));
-    b->n_hits_main = tot[0];
-    b->n_cig_main = tot[1];
-    if (copy) {   // otherwise the results stay in the pinned buffers (zero-copy view)
-        off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
-        hits.assign(b->h_pinned, b->h_pinned + tot[0]);
-        cig.assign(b->h_pinned_cig, b->h_pinned_cig + tot[1]);
-    }
+    if (n && tot[0])
+        HIPCHK(launch_pack(st, n, v, v, nullptr, b->off_hits, b->off_cig, d->ann_off, d->ann_id, b->d_out, b->d_out_cig,
+                           read_base, cig_base));
     return BSQ_OK;
 }
 
-// One workspace pass over reads [b->lo, b->lo + n): main pass, overflow retry, packing.  Results are left
-// in the pinned buffers (zero_copy) or in b->res_* (read_index / read_off local to the chunk).
-static int run_chunk(bsq_batch *b, const DOpts &o, int n, bool &zero_copy)
+// grows a pinned array to hold `need` elements, keeping the first `keep`
+template <typename T>
+static int grow_pinned(T *&p, int64_t &cap, int64_t need, int64_t keep)
+{
+    if (need <= cap) return BSQ_OK;
+    const int64_t nc = std::max<int64_t>(need, 2 * cap);
+    T *q = nullptr;
+    HIPCHK(hipHostMalloc((void **)&q, (size_t)nc * sizeof(T)));
+    if (keep > 0) memcpy(q, p, (size_t)keep * sizeof(T));
+    hipHostFree(p);
+    p = q;
+    cap = nc;
+    return BSQ_OK;
+}
+
+// Main-pass chunk [lo, lo + n): records land in the batch-wide pinned arrays at hit_dst / cig_dst with
+// batch-wide read indices and CIGAR offsets, read_off[lo .. lo + n] = batch-wide hit offsets.
+static int pack_main(bsq_batch *b, Workspace &w, int n, int lo, int64_t hit_dst, int64_t cig_dst, int64_t tot[2])
 {
     hipStream_t st = b->stream;
-    b->retried = 0;
+    { const int rc = pack_device(b, w, n, true, lo, cig_dst, tot); if (rc) return rc; }
+    { int rc = grow_pinned(b->h_pinned, b->h_cap, hit_dst + tot[0], hit_dst); if (rc) return rc; }
+    { int rc = grow_pinned(b->h_pinned_cig, b->h_cig_cap, cig_dst + tot[1], cig_dst); if (rc) return rc; }
+    { int rc = grow_pinned(b->h_pinned_off, b->h_off_cap, (int64_t)b->n_reads + 1, lo); if (rc) return rc; }
+    HIPCHK(launch_add_base(st, b->off_hits, n + 1, hit_dst));
+    HIPCHK(hipEventRecord(b->ev[STG_D2H], st));
+    HIPCHK(hipMemcpyAsync(b->h_pinned_off + lo, b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned + hit_dst, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
+    if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig + cig_dst, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(b->ev[STG_N], st));
+    HIPCHK(hipStreamSynchronize(st));
+    return BSQ_OK;
+}
+
+// Retry-pass chunk: records (chunk-local indices) into host vectors.
+static int pack_retry(bsq_batch *b, Workspace &w, int n, std::vector<bsq_hit> &hits, std::vector<uint32_t> &cig,
+                      std::vector<int64_t> &off)
+{
+    hipStream_t st = b->stream;
+    int64_t tot[2];
+    { const int rc = pack_device(b, w, n, false, 0, 0, tot); if (rc) return rc; }
+    off.resize((size_t)n + 1);
+    hits.resize((size_t)tot[0]);
+    cig.resize((size_t)tot[1]);
+    HIPCHK(hipMemcpyAsync(off.data(), b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (tot[0]) HIPCHK(hipMemcpyAsync(hits.data(), b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
+    if (tot[1]) HIPCHK(hipMemcpyAsync(cig.data(), b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return BSQ_OK;
+}
+
+// One workspace pass over reads [b->lo, b->lo + n): main pass, packing into the batch-wide pinned arrays
+// at (*hit_total, *cig_total), and the large-capacity retry for overflowing reads, merged in place.
+static int run_chunk(bsq_batch *b, const DOpts &o, int n, int64_t &hit_total, int64_t &cig_total)
+{
+    hipStream_t st = b->stream;
+    const int lo = b->lo;
     int rc = run_stages(b, b->main, o, n, nullptr, true);
     if (rc) return rc;
     // overflowing reads -> retry workspace with large capacities
@@ -752,79 +778,101 @@ static int run_chunk(bsq_batch *b, const DOpts &o, int n, bool &zero_copy)
     HIPCHK(launch_collect_overflow(st, n, b->main.status, b->ovf_list, b->ovf_count));
     int32_t novf = 0;
     HIPCHK(hipMemcpyAsync(&novf, b->ovf_count, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    rc = pack_to_host(b, b->main, n, true, b->res_hits, b->res_cig, b->res_off, true, /*copy=*/false);
+    int64_t tot[2];
+    rc = pack_main(b, b->main, n, lo, hit_total, cig_total, tot);
     if (rc) return rc;
-    zero_copy = novf == 0;
-    if (novf > 0) {
-        // the retry pass reuses the pinned buffers: keep the main results first
-        b->res_off.assign(b->h_pinned_off, b->h_pinned_off + n + 1);
-        b->res_hits.assign(b->h_pinned, b->h_pinned + b->n_hits_main);
-        b->res_cig.assign(b->h_pinned_cig, b->h_pinned_cig + b->n_cig_main);
-        b->retried = novf;
-        std::vector<int32_t> list((size_t)novf);
-        HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
-        std::sort(list.begin(), list.end());
-        const int CH = 256;
-        if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
-            b->retry.release();
-            rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
-            if (rc) return rc;
-        }
-        // per-read replacement results
-        std::vector<std::vector<bsq_hit>> rh((size_t)novf);
-        std::vector<std::vector<uint32_t>> rcg((size_t)novf);
-        for (int s = 0; s < novf; s += CH) {
-            int m = std::min(CH, novf - s);
-            HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
-            rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
-            if (rc) return rc;
-            std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
-            rc = pack_to_host(b, b->retry, m, false, hh, cc, oo, false);
-            if (rc) return rc;
-            for (int j = 0; j < m; ++j) {
-                auto &dst = rh[(size_t)(s + j)];
-                auto &dc = rcg[(size_t)(s + j)];
-                for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
-                    bsq_hit x = hh[(size_t)k];
-                    uint32_t base = (uint32_t)dc.size();
-                    dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
-                    x.cigar_off = base;
-                    dst.push_back(x);
-                }
-            }
-        }
-        // merge into read order
-        std::vector<bsq_hit> mh; std::vector<uint32_t> mc; std::vector<int64_t> mo((size_t)n + 1, 0);
-        size_t li = 0;
-        for (int r = 0; r < n; ++r) {
-            mo[r] = (int64_t)mh.size();
-            if (li < list.size() && list[li] == r) {
-                for (auto x : rh[li]) {
-                    uint32_t base = (uint32_t)mc.size();
-                    mc.insert(mc.end(), rcg[li].begin() + x.cigar_off, rcg[li].begin() + x.cigar_off + x.n_cigar);
-                    x.cigar_off = base; x.read_index = r;
-                    mh.push_back(x);
-                }
-                ++li;
-            } else {
-                for (int64_t k = b->res_off[r]; k < b->res_off[r + 1]; ++k) {
-                    bsq_hit x = b->res_hits[(size_t)k];
-                    uint32_t base = (uint32_t)mc.size();
-                    mc.insert(mc.end(), b->res_cig.begin() + x.cigar_off, b->res_cig.begin() + x.cigar_off + x.n_cigar);
-                    x.cigar_off = base;
-                    mh.push_back(x);
-                }
-            }
-        }
-        mo[n] = (int64_t)mh.size();
-        b->res_hits.swap(mh); b->res_cig.swap(mc); b->res_off.swap(mo);
-    }
-    for (int s = 0; s < STG_N; ++s) {   // per-chunk device time, summed over chunks
+    for (int s = 0; s < STG_N; ++s) {   // per-chunk device time (main pass), summed over chunks
         float ms = 0;
         hipEventElapsedTime(&ms, b->ev[s], b->ev[s + 1]);
         b->stage_ms[s] += ms;
     }
+    if (novf == 0) { hit_total += tot[0]; cig_total += tot[1]; return BSQ_OK; }
+
+    // chunk-local copy of the main results (the retry pass re-runs the pack machinery)
+    b->retried += novf;
+    b->main_off.resize((size_t)n + 1);
+    for (int r = 0; r <= n; ++r) b->main_off[r] = b->h_pinned_off[lo + r] - hit_total;
+    b->main_hits.assign(b->h_pinned + hit_total, b->h_pinned + hit_total + tot[0]);
+    for (auto &x : b->main_hits) { x.read_index -= lo; x.cigar_off -= (uint32_t)cig_total; }
+    b->main_cig.assign(b->h_pinned_cig + cig_total, b->h_pinned_cig + cig_total + tot[1]);
+    std::vector<int32_t> list((size_t)novf);
+    HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
+    std::sort(list.begin(), list.end());
+    const int CH = 256;
+    if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
+        b->retry.release();
+        rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
+        if (rc) return rc;
+    }
+    // per-read replacement results
+    std::vector<std::vector<bsq_hit>> rh((size_t)novf);
+    std::vector<std::vector<uint32_t>> rcg((size_t)novf);
+    for (int s = 0; s < novf; s += CH) {
+        int m = std::min(CH, novf - s);
+        HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
+        rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
+        if (rc) return rc;
+        std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
+        rc = pack_retry(b, b->retry, m, hh, cc, oo);
+        if (rc) return rc;
+        for (int j = 0; j < m; ++j) {
+            auto &dst = rh[(size_t)(s + j)];
+            auto &dc = rcg[(size_t)(s + j)];
+            for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
+                bsq_hit x = hh[(size_t)k];
+                uint32_t base = (uint32_t)dc.size();
+                dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
+                x.cigar_off = base;
+                dst.push_back(x);
+            }
+        }
+    }
+    // merge into read order (chunk-local): bulk copies of the runs of main-pass reads between retried ones
+    std::vector<bsq_hit> &mh = b->res_hits;
+    std::vector<uint32_t> &mc = b->res_cig;
+    std::vector<int64_t> &mo = b->res_off;
+    mh.clear(); mc.clear(); mo.assign((size_t)n + 1, 0);
+    const std::vector<int64_t> &MO = b->main_off;
+    auto copy_run = [&](int r0, int r1) {   // main-pass reads [r0, r1)
+        if (r0 >= r1) return;
+        const int64_t h0 = MO[r0], h1 = MO[r1], hb = (int64_t)mh.size();
+        for (int r = r0; r < r1; ++r) mo[r] = hb + (MO[r] - h0);
+        if (h1 == h0) return;
+        const uint32_t c0 = b->main_hits[h0].cigar_off;
+        const uint32_t c1 = b->main_hits[h1 - 1].cigar_off + b->main_hits[h1 - 1].n_cigar;
+        const uint32_t cb = (uint32_t)mc.size();
+        mh.insert(mh.end(), b->main_hits.begin() + h0, b->main_hits.begin() + h1);
+        for (int64_t k = hb; k < (int64_t)mh.size(); ++k) mh[k].cigar_off = mh[k].cigar_off - c0 + cb;
+        mc.insert(mc.end(), b->main_cig.begin() + c0, b->main_cig.begin() + c1);
+    };
+    int prev = 0;
+    for (size_t li = 0; li < list.size(); ++li) {
+        const int r = list[li];
+        copy_run(prev, r);
+        mo[r] = (int64_t)mh.size();
+        for (auto x : rh[li]) {
+            uint32_t base = (uint32_t)mc.size();
+            mc.insert(mc.end(), rcg[li].begin() + x.cigar_off, rcg[li].begin() + x.cigar_off + x.n_cigar);
+            x.cigar_off = base; x.read_index = r;
+            mh.push_back(x);
+        }
+        prev = r + 1;
+    }
+    copy_run(prev, n);
+    mo[n] = (int64_t)mh.size();
+    // write the merged chunk back into the batch-wide pinned arrays
+    { int rc2 = grow_pinned(b->h_pinned, b->h_cap, hit_total + (int64_t)mh.size(), hit_total); if (rc2) return rc2; }
+    { int rc2 = grow_pinned(b->h_pinned_cig, b->h_cig_cap, cig_total + (int64_t)mc.size(), cig_total); if (rc2) return rc2; }
+    for (size_t k = 0; k < mh.size(); ++k) {
+        bsq_hit x = mh[k];
+        x.read_index += lo;
+        x.cigar_off += (uint32_t)cig_total;
+        b->h_pinned[hit_total + (int64_t)k] = x;
+    }
+    if (!mc.empty()) memcpy(b->h_pinned_cig + cig_total, mc.data(), mc.size() * 4);
+    for (int r = 0; r <= n; ++r) b->h_pinned_off[lo + r] = hit_total + mo[r];
+    hit_total += (int64_t)mh.size();
+    cig_total += (int64_t)mc.size();
     return BSQ_OK;
 }
 
@@ -848,48 +896,18 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, st));
     b->retried = 0;
-    b->res_hits.clear(); b->res_cig.clear(); b->res_off.assign((size_t)n + 1, 0);
     int rc = BSQ_OK;
-    bool zero_copy = false;
     for (int s = 0; s < STG_N; ++s) b->stage_ms[s] = 0;
+    { const int rc2 = grow_pinned(b->h_pinned_off, b->h_off_cap, (int64_t)n + 1, 0); if (rc2) return rc2; }
+    int64_t hit_total = 0, cig_total = 0;
     if (n > 0 && b->idx->h.seq_len > 0) {
-        if (n <= b->chunk) {
+        // workspace-sized chunks; every chunk's records land in place in the batch-wide pinned arrays
+        for (int lo = 0; lo < n; lo += b->chunk) {
+            const int m = std::min(b->chunk, n - lo);
+            b->lo = lo;
+            rc = run_chunk(b, o, m, hit_total, cig_total);
             b->lo = 0;
-            rc = run_chunk(b, o, n, zero_copy);
             if (rc) return rc;
-        } else {   // chunks of the workspace size, results appended in read order
-            std::vector<bsq_hit> H;
-            std::vector<uint32_t> G;
-            std::vector<int64_t> F((size_t)n + 1, 0);
-            int64_t retried = 0;
-            for (int lo = 0; lo < n; lo += b->chunk) {
-                const int m = std::min(b->chunk, n - lo);
-                bool zc = false;
-                b->lo = lo;
-                rc = run_chunk(b, o, m, zc);
-                b->lo = 0;
-                if (rc) return rc;
-                retried += b->retried;
-                const bsq_hit *hp = zc ? b->h_pinned : b->res_hits.data();
-                const uint32_t *cp = zc ? b->h_pinned_cig : b->res_cig.data();
-                const int64_t *op = zc ? b->h_pinned_off : b->res_off.data();
-                const int64_t nh = zc ? b->n_hits_main : (int64_t)b->res_hits.size();
-                const int64_t nc = zc ? b->n_cig_main : (int64_t)b->res_cig.size();
-                const int64_t hbase = (int64_t)H.size();
-                const uint32_t cbase = (uint32_t)G.size();
-                for (int r = 0; r < m; ++r) F[(size_t)lo + r] = hbase + op[r];
-                for (int64_t k = 0; k < nh; ++k) {
-                    bsq_hit x = hp[k];
-                    x.read_index += lo;
-                    x.cigar_off += cbase;
-                    H.push_back(x);
-                }
-                G.insert(G.end(), cp, cp + nc);
-            }
-            F[(size_t)n] = (int64_t)H.size();
-            b->res_hits.swap(H); b->res_cig.swap(G); b->res_off.swap(F);
-            b->retried = retried;
-            zero_copy = false;
         }
         // algorithmic bytes (stage times were summed over the chunks)
         Counters c[STG_N];
@@ -899,28 +917,21 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_CHAIN] = 8.0 * c[STG_CHAIN].sa_values;
         b->stage_bytes[STG_EXTEND] = (double)c[STG_EXTEND].ref_bases;
         b->stage_bytes[STG_REG2ALN] = (double)c[STG_REG2ALN].ref_bases;
-        b->stage_bytes[STG_PACK] = zero_copy ? (double)b->n_hits_main * sizeof(bsq_hit) + 4.0 * b->n_cig_main
-                                             : (double)b->res_hits.size() * sizeof(bsq_hit) + 4.0 * b->res_cig.size();
+        b->stage_bytes[STG_PACK] = (double)hit_total * sizeof(bsq_hit) + 4.0 * (double)cig_total;
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
     } else {
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
+    // the results stay in the batch-wide pinned arrays (zero-copy view, valid until the next run)
+    if (n == 0 || b->idx->h.seq_len == 0) for (int r = 0; r <= n; ++r) b->h_pinned_off[r] = 0;
     b->view.n_reads = n;
-    if (zero_copy) {
-        b->view.n_hits = b->n_hits_main;
-        b->view.hits = b->h_pinned;
-        b->view.read_off = b->h_pinned_off;
-        b->view.n_cigar = b->n_cig_main;
-        b->view.cigar = b->h_pinned_cig;
-    } else {
-        b->view.n_hits = (int64_t)b->res_hits.size();
-        b->view.hits = b->res_hits.data();
-        b->view.read_off = b->res_off.data();
-        b->view.n_cigar = (int64_t)b->res_cig.size();
-        b->view.cigar = b->res_cig.data();
-    }
+    b->view.n_hits = hit_total;
+    b->view.hits = b->h_pinned;
+    b->view.read_off = b->h_pinned_off;
+    b->view.n_cigar = cig_total;
+    b->view.cigar = b->h_pinned_cig;
     return BSQ_OK;
 }
 

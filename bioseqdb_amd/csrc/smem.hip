@@ -26,6 +26,18 @@ struct FM {
     const OccBlock32 *occ32;   // 64-base blocks, used when X is u32
     const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
     int K;
+    // table entry idx: (x[0], x[1], x[2]) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B)
+    DEV void kget(uint32_t idx, X &a0, X &a1, X &a2) const
+    {
+        if constexpr (sizeof(X) == 4) {
+            const uint4 e = kt[idx];
+            a0 = e.x; a1 = e.y; a2 = e.z;
+        } else {
+            const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(kt) + 2 * (size_t)idx;
+            const ulonglong2 u = p[0], v = p[1];
+            a0 = u.x; a1 = u.y; a2 = v.x;
+        }
+    }
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
     DEV X L2(int c) const { return c == 0 ? l2_0 : c == 1 ? l2_1 : c == 2 ? l2_2 : c == 3 ? l2_3 : l2_4; }
 };
@@ -221,8 +233,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
             X n1, n0, n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
-                const uint4 e = fm.kt[koff(i - x + 1) + fcode];
-                n0 = (X)e.x; n1 = (X)e.y; n2 = (X)e.z;
+                fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 != ik2) {
@@ -273,13 +284,13 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
                 // strings q[i .. end) of at most K bases come from the k-mer table
                 const int La = pae - i, Lb = pbe - i;
                 const bool ta = La <= K, tb = hb && Lb <= K;
-                uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
-                if (ta) ea = fm.kt[koff(La) + (wcode >> (2 * (K - La)))];
-                if (tb) eb = fm.kt[koff(Lb) + (wcode >> (2 * (K - Lb)))];
+                X ea0 = 0, ea1 = 0, ea2 = 0, eb0 = 0, eb1 = 0, eb2 = 0;
+                if (ta) fm.kget(koff(La) + (wcode >> (2 * (K - La))), ea0, ea1, ea2);
+                if (tb) fm.kget(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb1, eb2);
                 nkm += (uint64_t)ta + (uint64_t)tb;
                 if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
-                if (ta) { oa0 = (X)ea.x; oa2 = (X)ea.z; }
-                if (tb) { ob0 = (X)eb.x; ob2 = (X)eb.z; }
+                if (ta) { oa0 = ea0; oa2 = ea2; }
+                if (tb) { ob0 = eb0; ob2 = eb2; }
             }
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && !hb) break;
@@ -325,8 +336,7 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, const uint8_t *q, int x, int 
             X n1, n0, n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
-                const uint4 e = fm.kt[koff(i - x + 1) + fcode];
-                n0 = (X)e.x; n1 = (X)e.y; n2 = (X)e.z;
+                fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 < (X)max_intv && i - x >= min_len) {
@@ -372,7 +382,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
-    fm.K = sizeof(X) == 4 ? ix.kmer_k : 0;
+    fm.K = ix.kmer_k;   // the table is built in the index's row width
     uint64_t nblk = 0, nkm = 0;
     const int li = blockIdx.x * T + t;
     if (li < n) {
@@ -774,53 +784,63 @@ hipError_t launch_smem_flat(hipStream_t st, const DIndex &ix, const DOpts &o, co
 // bidirectional interval of a string does not depend on the extension path that reached it, so a
 // table entry equals what the kernels' forward or backward extend chains compute for that string
 // (only non-empty intervals are ever consumed; empty ones are only compared against x[2] bounds).
-__global__ void k_kmer_level(DIndex ix, uint4 *tab, int L)
+template <typename X>
+__global__ void k_kmer_level(DIndex ix, void *tabv, int L)
 {
     const uint64_t n = 1ull << (2 * L);
     const uint64_t P = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    auto put = [&](uint64_t idx, X a0, X a1, X a2) {
+        if constexpr (sizeof(X) == 4) {
+            reinterpret_cast<uint4 *>(tabv)[idx] = make_uint4(a0, a1, a2, 0u);
+        } else {
+            ulonglong2 *p = reinterpret_cast<ulonglong2 *>(tabv) + 2 * idx;
+            p[0] = make_ulonglong2(a0, a1);
+            p[1] = make_ulonglong2(a2, 0ull);
+        }
+    };
     if (L == 0) {
         if (P < 4) {
             const int c = (int)P;
-            tab[P] = make_uint4((uint32_t)ix.L2[c] + 1, (uint32_t)ix.L2[3 - c] + 1,
-                                (uint32_t)(ix.L2[c + 1] - ix.L2[c]), 0u);
+            put(P, (X)ix.L2[c] + 1, (X)ix.L2[3 - c] + 1, (X)(ix.L2[c + 1] - ix.L2[c]));
         }
         return;
     }
     if (P >= n) return;
-    FM<uint32_t> fm;
+    FM<X> fm;
     fm.occ = ix.occ;
     fm.occ32 = ix.occ32;
-    fm.kt = nullptr;
+    fm.kt = reinterpret_cast<const uint4 *>(tabv);
     fm.K = 0;
-    fm.l2_0 = (uint32_t)ix.L2[0]; fm.l2_1 = (uint32_t)ix.L2[1]; fm.l2_2 = (uint32_t)ix.L2[2];
-    fm.l2_3 = (uint32_t)ix.L2[3]; fm.l2_4 = (uint32_t)ix.L2[4];
-    fm.primary = (uint32_t)ix.primary;
-    const uint4 e = tab[koff(L) + P];
-    const uint32_t x0 = e.x, x1 = e.y, x2 = e.z;
-    uint32_t o0[4], o2[4];
+    fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2];
+    fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
+    fm.primary = (X)ix.primary;
+    X x0, x1, x2;
+    fm.kget((uint32_t)(koff(L) + P), x0, x1, x2);
+    X o0[4], o2[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t na, no, nx2;
+        X na, no, nx2;
         uint64_t nb = 0;
-        extend1(fm, x0, 0u, x2, c, na, no, nx2, nb);
+        extend1(fm, x0, (X)0, x2, c, na, no, nx2, nb);
         o0[c] = na; o2[c] = nx2;
     }
-    const uint32_t x1_3 = x1 + (uint32_t)(x0 <= fm.primary && x0 + x2 - 1 >= fm.primary);
-    const uint32_t x1_2 = x1_3 + o2[3], x1_1 = x1_2 + o2[2], x1_0 = x1_1 + o2[1];
-    uint4 *dst = tab + koff(L + 1) + P;
-    dst[0 * n] = make_uint4(o0[0], x1_0, o2[0], 0u);
-    dst[1 * n] = make_uint4(o0[1], x1_1, o2[1], 0u);
-    dst[2 * n] = make_uint4(o0[2], x1_2, o2[2], 0u);
-    dst[3 * n] = make_uint4(o0[3], x1_3, o2[3], 0u);
+    const X x1_3 = x1 + (X)(x0 <= fm.primary && x0 + x2 - 1 >= fm.primary);
+    const X x1_2 = x1_3 + o2[3], x1_1 = x1_2 + o2[2], x1_0 = x1_1 + o2[1];
+    const uint64_t d = koff(L + 1) + P;
+    put(d + 0 * n, o0[0], x1_0, o2[0]);
+    put(d + 1 * n, o0[1], x1_1, o2[1]);
+    put(d + 2 * n, o0[2], x1_2, o2[2]);
+    put(d + 3 * n, o0[3], x1_3, o2[3]);
 }
 
+// entry bytes: 16 (u32 rows) or 32 (64-bit rows)
 hipError_t launch_kmer_build(hipStream_t st, const DIndex &ix, uint32_t *tab, int K)
 {
-    uint4 *t = reinterpret_cast<uint4 *>(tab);
-    hipLaunchKernelGGL(k_kmer_level, dim3(1), dim3(64), 0, st, ix, t, 0);
-    for (int L = 1; L < K; ++L) {
-        const uint64_t n = 1ull << (2 * L);
-        hipLaunchKernelGGL(k_kmer_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, t, L);
+    for (int L = 0; L < K; ++L) {
+        const uint64_t n = L == 0 ? 4 : 1ull << (2 * L);
+        const dim3 g((unsigned)((n + 255) / 256)), bl(256);
+        if (ix.wide) hipLaunchKernelGGL(k_kmer_level<uint64_t>, g, bl, 0, st, ix, (void *)tab, L);
+        else hipLaunchKernelGGL(k_kmer_level<uint32_t>, g, bl, 0, st, ix, (void *)tab, L);
     }
     return hipGetLastError();
 }
