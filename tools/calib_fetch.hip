@@ -45,6 +45,34 @@ __global__ void k_gather16(const uint4 *t, uint64_t nent, uint64_t nlanes, uint3
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+__global__ void k_copy(const uint4 *a, uint4 *b, uint64_t n16)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
+// STREAM-like ceilings: 2 GiB read-only stream and a 2 GiB -> 2 GiB copy, best of 5
+static void ceilings(uint4 *t, uint32_t *sink)
+{
+    const uint64_t bytes = 2ull << 30, n16 = bytes / 16;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    float best_r = 1e30f, best_c = 1e30f;
+    for (int it = 0; it < 5; ++it) {
+        float ms = 0;
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(k_stream, dim3(8192), dim3(256), 0, 0, t, n16, sink);
+        hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms, e0, e1);
+        best_r = ms < best_r ? ms : best_r;
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, t, t + n16, n16);
+        hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms, e0, e1);
+        best_c = ms < best_c ? ms : best_c;
+    }
+    printf("ceiling: stream-read %.0f GB/s, copy %.0f GB/s (read+write bytes), 2 GiB each\n",
+           bytes / (best_r * 1e-3) / 1e9, 2.0 * bytes / (best_c * 1e-3) / 1e9);
+}
+
 int main()
 {
     const uint64_t big = 4ull << 30, small = 96ull << 20, bytes = 1ull << 30;
@@ -62,6 +90,7 @@ int main()
     hipLaunchKernelGGL(k_gather64, dim3((unsigned)(n64 / 256)), dim3(256), 0, 0, t, small / 64, n64, sink);
     hipLaunchKernelGGL(k_gather16, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, t, small / 16, n16, sink);
     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
+    ceilings(t, sink);
     printf("dispatch order: stream(4G) gather64(4G) gather16(4G) stream(96M warm) gather64(96M) gather16(96M); "
            "each reads %llu bytes except the warm stream (%llu)\n", (unsigned long long)bytes, (unsigned long long)small);
     return 0;
