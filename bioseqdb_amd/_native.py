@@ -47,6 +47,13 @@ class Hit(ctypes.Structure):
     ]
 
 
+class Table(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("bytes", ctypes.c_uint64)]
+
+
+N_TABLES = 8
+
+
 class Hits(ctypes.Structure):
     _fields_ = [
         ("n_reads", ctypes.c_int32), ("n_hits", ctypes.c_int64), ("hits", ctypes.POINTER(Hit)),
@@ -91,6 +98,9 @@ SIGNATURES = {
     "bsq_batch_stage_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "bsq_batch_stage_work": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "bsq_batch_seed": (ctypes.c_int, [_P, _P]),
+    "bsq_index_layout": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _P, ctypes.POINTER(ctypes.c_uint64)]),
+    "bsq_index_upload_into": (ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int]),
+    "bsq_index_import": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, _P, ctypes.c_int, ctypes.POINTER(_P)]),
     "bsq_batch_intervals": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(ctypes.c_int64)),
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                            ctypes.POINTER(ctypes.c_int64)]),

@@ -119,9 +119,11 @@ struct DeviceIndex {
     int32_t *ann_len = nullptr;
     uint32_t *kmer = nullptr;
     OccBlock32 *occ32 = nullptr;
+    bool owned = true;   // false: the tables live in caller-owned buffers (bsq_index_upload_into / _import)
     DIndex view{};
     ~DeviceIndex()
     {
+        if (!owned) return;
         if (device >= 0) hipSetDevice(device);
         hipFree(occ); hipFree(sa); hipFree(pac); hipFree(ann_off); hipFree(ann_id); hipFree(ann_len); hipFree(kmer); hipFree(occ32);
     }
@@ -195,57 +197,120 @@ extern "C" const void *bsq_index_sa_data(const bsq_index *idx, int *elem_bytes)
     return idx->h.sa64.data();
 }
 
-extern "C" int bsq_index_upload(bsq_index *idx, int device)
+// ---- device tables of an index (bsq_index_layout order) and the metadata that travels with them ----
+enum { T_OCC = 0, T_OCC32, T_SA, T_PAC, T_ANN_OFF, T_ANN_ID, T_ANN_LEN, T_KMER, T_N };
+static_assert(T_N == BSQ_N_TABLES, "table list");
+
+struct IndexMeta {   // fixed header of the metadata blob; followed by Ann[n_anns] and Hole[n_holes]
+    char magic[8];
+    uint64_t l_pac, seq_len, primary, L2[5];
+    int32_t wide, kmer_k;
+    uint64_t n_anns, n_holes, pac_bytes;
+    uint64_t table_bytes[T_N];
+};
+
+static int kmer_depth(uint64_t seq_len)
+{
+    if (seq_len == 0) return 0;
+    int K = 0;
+    while (K < 11 && (1ull << (2 * (K + 1))) <= seq_len) ++K;   // ~log4(rows), at most 11
+    if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
+    return K;
+}
+
+static void table_sizes(const HostIndex &h, uint64_t bytes[T_N], int &K, int &wide)
+{
+    for (int t = 0; t < T_N; ++t) bytes[t] = 0;
+    wide = h.sa32.empty() ? 1 : 0;
+    const uint64_t nann = h.anns.size() ? h.anns.size() : 1;
+    bytes[T_ANN_OFF] = nann * 8; bytes[T_ANN_ID] = nann * 8; bytes[T_ANN_LEN] = nann * 4;
+    K = 0;
+    if (h.seq_len == 0) return;
+    bytes[T_OCC] = h.occ.size() * sizeof(OccBlock);
+    bytes[T_OCC32] = wide ? 0 : h.occ.size() * 2 * sizeof(OccBlock32);
+    bytes[T_SA] = wide ? h.sa64.size() * 8 : h.sa32.size() * 4;
+    bytes[T_PAC] = h.pac.size() + 16;
+    K = kmer_depth(h.seq_len);
+    bytes[T_KMER] = K ? (((uint64_t)1 << (2 * (K + 1))) - 4) / 3 * (wide ? 32 : 16) : 0;
+}
+
+static void set_view(DeviceIndex *d, const IndexMeta &m)
+{
+    DIndex &v = d->view;
+    v = DIndex{};
+    v.occ = d->occ;
+    v.sa32 = m.wide ? nullptr : (const uint32_t *)d->sa;
+    v.sa64 = m.wide ? (const uint64_t *)d->sa : nullptr;
+    v.pac = d->pac;
+    v.ann_off = d->ann_off;
+    v.ann_len = d->ann_len;
+    v.n_anns = (int32_t)m.n_anns;
+    for (int c = 0; c < 5; ++c) v.L2[c] = m.L2[c];
+    v.primary = m.primary;
+    v.seq_len = m.seq_len;
+    v.l_pac = (int64_t)m.l_pac;
+    v.wide = m.wide;
+    v.occ32 = m.wide ? nullptr : d->occ32;
+    v.kmer = m.kmer_k ? d->kmer : nullptr;
+    v.kmer_k = m.kmer_k;
+}
+
+static IndexMeta meta_of(const HostIndex &h)
+{
+    IndexMeta m{};
+    memcpy(m.magic, "BSQIDX1", 8);
+    m.l_pac = (uint64_t)h.l_pac; m.seq_len = h.seq_len; m.primary = h.primary;
+    for (int c = 0; c < 5; ++c) m.L2[c] = h.L2[c];
+    int K = 0, wide = 0;
+    table_sizes(h, m.table_bytes, K, wide);
+    m.wide = wide; m.kmer_k = K;
+    m.n_anns = h.anns.size(); m.n_holes = h.holes.size(); m.pac_bytes = h.pac.size();
+    return m;
+}
+
+// Uploads the host index into its own allocations (ext == nullptr) or into caller-owned buffers.
+static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
 {
     if (!idx || !idx->h.built) { set_err("index not built"); return BSQ_E_INVALID; }
+    const HostIndex &h = idx->h;
+    if (h.seq_len > 0 && h.occ.empty()) { set_err("device-only index (imported): nothing to upload from the host"); return BSQ_E_INVALID; }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
         set_err("no HIP device %d (found %d); the alignment path has no CPU fallback", device, ndev);
         return BSQ_E_NODEV;
     }
     HIPCHK(hipSetDevice(device));
+    const IndexMeta m = meta_of(h);
+    void *ptr[T_N] = {};
+    for (int t = 0; t < T_N; ++t) {
+        if (!m.table_bytes[t]) continue;
+        if (ext) {
+            if (!ext[t].ptr || ext[t].bytes < m.table_bytes[t]) { set_err("table %d: buffer of %llu bytes, %llu needed", t,
+                (unsigned long long)ext[t].bytes, (unsigned long long)m.table_bytes[t]); return BSQ_E_INVALID; }
+            ptr[t] = ext[t].ptr;
+        } else HIPCHK(hipMalloc(&ptr[t], m.table_bytes[t]));
+    }
     delete idx->h.dev;
-    idx->h.dev = new DeviceIndex();
-    DeviceIndex *d = idx->h.dev;
+    DeviceIndex *d = idx->h.dev = new DeviceIndex();
     d->device = device;
-    const HostIndex &h = idx->h;
+    d->owned = ext == nullptr;
+    d->occ = (OccBlock *)ptr[T_OCC]; d->occ32 = (OccBlock32 *)ptr[T_OCC32]; d->sa = ptr[T_SA];
+    d->pac = (uint8_t *)ptr[T_PAC]; d->ann_off = (int64_t *)ptr[T_ANN_OFF]; d->ann_id = (int64_t *)ptr[T_ANN_ID];
+    d->ann_len = (int32_t *)ptr[T_ANN_LEN]; d->kmer = (uint32_t *)ptr[T_KMER];
     const size_t nann = h.anns.size() ? h.anns.size() : 1;
     std::vector<int64_t> off(nann, 0), id(nann, 0);
     std::vector<int32_t> len(nann, 0);
     for (size_t i = 0; i < h.anns.size(); ++i) { off[i] = h.anns[i].offset; id[i] = h.anns[i].id; len[i] = h.anns[i].len; }
-    HIPCHK(hipMalloc(&d->ann_off, nann * 8));
-    HIPCHK(hipMalloc(&d->ann_id, nann * 8));
-    HIPCHK(hipMalloc(&d->ann_len, nann * 4));
     HIPCHK(hipMemcpy(d->ann_off, off.data(), nann * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->ann_id, id.data(), nann * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->ann_len, len.data(), nann * 4, hipMemcpyHostToDevice));
     if (h.seq_len > 0) {
-        HIPCHK(hipMalloc(&d->occ, h.occ.size() * sizeof(OccBlock)));
         HIPCHK(hipMemcpy(d->occ, h.occ.data(), h.occ.size() * sizeof(OccBlock), hipMemcpyHostToDevice));
-        size_t sab = h.sa32.empty() ? h.sa64.size() * 8 : h.sa32.size() * 4;
-        HIPCHK(hipMalloc(&d->sa, sab));
-        HIPCHK(hipMemcpy(d->sa, h.sa32.empty() ? (const void *)h.sa64.data() : (const void *)h.sa32.data(), sab,
+        HIPCHK(hipMemcpy(d->sa, m.wide ? (const void *)h.sa64.data() : (const void *)h.sa32.data(), m.table_bytes[T_SA],
                          hipMemcpyHostToDevice));
-        HIPCHK(hipMalloc(&d->pac, h.pac.size() + 16));
         HIPCHK(hipMemcpy(d->pac, h.pac.data(), h.pac.size(), hipMemcpyHostToDevice));
     }
-    DIndex &v = d->view;
-    v.occ = d->occ;
-    v.sa32 = h.sa32.empty() ? nullptr : (const uint32_t *)d->sa;
-    v.sa64 = h.sa32.empty() ? (const uint64_t *)d->sa : nullptr;
-    v.pac = d->pac;
-    v.ann_off = d->ann_off;
-    v.ann_len = d->ann_len;
-    v.n_anns = (int32_t)h.anns.size();
-    for (int c = 0; c < 5; ++c) v.L2[c] = h.L2[c];
-    v.primary = h.primary;
-    v.seq_len = h.seq_len;
-    v.l_pac = h.l_pac;
-    v.kmer = nullptr;
-    v.kmer_k = 0;
-    v.occ32 = nullptr;
-    v.wide = h.sa32.empty() ? 1 : 0;
-    if (h.seq_len > 0 && !v.wide) {
+    if (h.seq_len > 0 && !m.wide) {
         // 64-base blocks: half 0 of each 128-base block keeps its counts, half 1 adds the first 64 bases
         std::vector<OccBlock32> o32(h.occ.size() * 2);
         for (size_t b = 0; b < h.occ.size(); ++b) {
@@ -260,25 +325,92 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device)
             c.cnt[2] = (uint32_t)B.cnt[2] + n2; c.cnt[3] = (uint32_t)B.cnt[3] + n3;
             c.hi = B.hi[1]; c.lo = B.lo[1];
         }
-        HIPCHK(hipMalloc(&d->occ32, o32.size() * sizeof(OccBlock32)));
         HIPCHK(hipMemcpy(d->occ32, o32.data(), o32.size() * sizeof(OccBlock32), hipMemcpyHostToDevice));
-        v.occ32 = d->occ32;
     }
-    // k-mer interval table: depth ~log4(rows), at most 11 (u32 rows: 89 MB, stays in the Infinity Cache
-    // beside the occ array at 100 Mbp; 64-bit rows: 32-B entries, 179 MB); BSQ_KMER_K overrides, 0 disables
-    if (h.seq_len > 0) {
-        int K = 0;
-        while (K < 11 && (1ull << (2 * (K + 1))) <= h.seq_len) ++K;
-        if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
-        if (K > 0) {
-            const size_t entries = (((size_t)1 << (2 * (K + 1))) - 4) / 3;
-            HIPCHK(hipMalloc(&d->kmer, entries * (v.wide ? 32 : 16)));
-            v.kmer = d->kmer;
-            HIPCHK(launch_kmer_build(nullptr, v, d->kmer, K));
-            HIPCHK(hipDeviceSynchronize());
-            v.kmer_k = K;
-        }
+    IndexMeta mv = m;
+    mv.kmer_k = 0;
+    set_view(d, mv);
+    // k-mer interval table (u32 rows: 89 MB at K = 11, stays in the Infinity Cache beside the occ array at
+    // 100 Mbp; 64-bit rows: 32-B entries, 179 MB); BSQ_KMER_K overrides, 0 disables
+    if (m.kmer_k > 0) {
+        d->view.kmer = d->kmer;
+        HIPCHK(launch_kmer_build(nullptr, d->view, d->kmer, m.kmer_k));
+        HIPCHK(hipDeviceSynchronize());
+        d->view.kmer_k = m.kmer_k;
     }
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_upload(bsq_index *idx, int device) { return upload_impl(idx, device, nullptr); }
+
+extern "C" int bsq_index_layout(const bsq_index *idx, uint64_t *bytes, void *meta, uint64_t *meta_bytes)
+{
+    if (!idx || !idx->h.built || !meta_bytes) { set_err("index not built / invalid argument"); return BSQ_E_INVALID; }
+    const HostIndex &h = idx->h;
+    if (h.seq_len > 0 && h.occ.empty()) { set_err("device-only index (imported) has no host layout"); return BSQ_E_INVALID; }
+    const IndexMeta m = meta_of(h);
+    if (bytes) for (int t = 0; t < T_N; ++t) bytes[t] = m.table_bytes[t];
+    const uint64_t need = sizeof(IndexMeta) + h.anns.size() * sizeof(Ann) + h.holes.size() * sizeof(Hole);
+    if (meta) {
+        if (*meta_bytes < need) { set_err("metadata buffer of %llu bytes, %llu needed", (unsigned long long)*meta_bytes,
+                                          (unsigned long long)need); return BSQ_E_INVALID; }
+        uint8_t *p = (uint8_t *)meta;
+        memcpy(p, &m, sizeof m); p += sizeof m;
+        if (!h.anns.empty()) { memcpy(p, h.anns.data(), h.anns.size() * sizeof(Ann)); p += h.anns.size() * sizeof(Ann); }
+        if (!h.holes.empty()) memcpy(p, h.holes.data(), h.holes.size() * sizeof(Hole));
+    }
+    *meta_bytes = need;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_upload_into(bsq_index *idx, int device, const bsq_table *tables, int n_tables)
+{
+    if (!tables || n_tables != BSQ_N_TABLES) { set_err("expected %d tables", BSQ_N_TABLES); return BSQ_E_INVALID; }
+    return upload_impl(idx, device, tables);
+}
+
+extern "C" int bsq_index_import(const void *meta, uint64_t meta_bytes, int device, const bsq_table *tables, int n_tables,
+                                bsq_index **out)
+{
+    if (!meta || !out || !tables || n_tables != BSQ_N_TABLES || meta_bytes < sizeof(IndexMeta)) {
+        set_err("invalid argument"); return BSQ_E_INVALID;
+    }
+    IndexMeta m;
+    memcpy(&m, meta, sizeof m);
+    if (memcmp(m.magic, "BSQIDX1", 8) != 0) { set_err("not an index metadata blob"); return BSQ_E_INVALID; }
+    if (meta_bytes != sizeof m + m.n_anns * sizeof(Ann) + m.n_holes * sizeof(Hole)) { set_err("metadata size mismatch"); return BSQ_E_INVALID; }
+    for (int t = 0; t < T_N; ++t)
+        if (m.table_bytes[t] && (!tables[t].ptr || tables[t].bytes < m.table_bytes[t])) { set_err("table %d missing or short", t); return BSQ_E_INVALID; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+        set_err("no HIP device %d (found %d); the alignment path has no CPU fallback", device, ndev);
+        return BSQ_E_NODEV;
+    }
+    HIPCHK(hipSetDevice(device));
+    bsq_index *idx = new (std::nothrow) bsq_index();
+    if (!idx) { set_err("out of memory"); return BSQ_E_NOMEM; }
+    HostIndex &h = idx->h;
+    const uint8_t *p = (const uint8_t *)meta + sizeof m;
+    h.anns.resize(m.n_anns);
+    if (m.n_anns) { memcpy(h.anns.data(), p, m.n_anns * sizeof(Ann)); p += m.n_anns * sizeof(Ann); }
+    h.holes.resize(m.n_holes);
+    if (m.n_holes) memcpy(h.holes.data(), p, m.n_holes * sizeof(Hole));
+    h.l_pac = (int64_t)m.l_pac; h.seq_len = m.seq_len; h.primary = m.primary;
+    for (int c = 0; c < 5; ++c) h.L2[c] = m.L2[c];
+    h.pac.resize(m.pac_bytes);   // host copy for rendering (extract_reference_subseq)
+    if (m.pac_bytes && hipMemcpy(h.pac.data(), tables[T_PAC].ptr, m.pac_bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        delete idx; set_err("reading the broadcast pac"); return BSQ_E_HIP;
+    }
+    h.built = true;
+    DeviceIndex *d = h.dev = new DeviceIndex();
+    d->device = device;
+    d->owned = false;
+    d->occ = (OccBlock *)tables[T_OCC].ptr; d->occ32 = (OccBlock32 *)tables[T_OCC32].ptr; d->sa = tables[T_SA].ptr;
+    d->pac = (uint8_t *)tables[T_PAC].ptr; d->ann_off = (int64_t *)tables[T_ANN_OFF].ptr;
+    d->ann_id = (int64_t *)tables[T_ANN_ID].ptr; d->ann_len = (int32_t *)tables[T_ANN_LEN].ptr;
+    d->kmer = (uint32_t *)tables[T_KMER].ptr;
+    set_view(d, m);
+    *out = idx;
     return BSQ_OK;
 }
 

@@ -50,6 +50,48 @@ def gather_records(local: np.ndarray, group=None, device=None, dst: int = 0) -> 
     return [o[:s].cpu().numpy() for o, s in zip(out, sizes_i)]
 
 
+def replicate_index(L, idx, gpu: int, src: int = 0, group=None):
+    """One index build for the whole job: rank `src` passes its built host index
+    `idx`, every other rank passes None.  The root uploads into torch-allocated device buffers, the
+    metadata blob and every device table are broadcast (RCCL over xGMI with the "nccl" backend), and the
+    other ranks import them.  Returns (index handle, buffers to keep alive while the index is used)."""
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    from ._native import N_TABLES, Table, check
+
+    rank = dist.get_rank(group)
+    if rank == src:
+        sizes = (ctypes.c_uint64 * N_TABLES)()
+        mb = ctypes.c_uint64()
+        check(L.bsq_index_layout(idx, sizes, None, ctypes.byref(mb)))
+        meta = ctypes.create_string_buffer(mb.value)
+        check(L.bsq_index_layout(idx, sizes, meta, ctypes.byref(mb)))
+        obj = [list(sizes), bytes(meta.raw)]
+    else:
+        obj = [None, None]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    sizes, meta = obj
+    dev = torch.device("cuda", gpu)
+    bufs = [torch.empty(int(b), dtype=torch.uint8, device=dev) if b else None for b in sizes]
+    tables = (Table * N_TABLES)(*[Table(t.data_ptr() if t is not None else None, int(b)) for t, b in zip(bufs, sizes)])
+    if rank == src:
+        check(L.bsq_index_upload_into(idx, gpu, tables, N_TABLES))
+    torch.cuda.synchronize(dev)
+    for t in bufs:
+        if t is not None:
+            dist.broadcast(t, src=src, group=group)
+    torch.cuda.synchronize(dev)
+    if rank != src:
+        out = ctypes.c_void_p()
+        mbuf = ctypes.create_string_buffer(meta, len(meta))
+        check(L.bsq_index_import(mbuf, len(meta), gpu, tables, N_TABLES, ctypes.byref(out)))
+        idx = out
+    return idx, bufs
+
+
 def merge_rows(per_rank: Sequence[Sequence[tuple]]) -> List[tuple]:
     """Concatenate per-rank result rows in rank (= read) order."""
     out: List[tuple] = []

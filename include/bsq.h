@@ -110,6 +110,23 @@ int bsq_index_occ4(const bsq_index *idx, int64_t k, uint64_t cnt[4]);
 /* Export the full suffix array (seq_len+1 entries of `*elem_bytes` = 4 or 8 bytes); borrowed. */
 const void *bsq_index_sa_data(const bsq_index *idx, int *elem_bytes);
 
+/* ---- Index replication (one process per GPU, the index built once and broadcast
+ * over xGMI).  The device tables are plain byte buffers, so any collective can move them: the root builds,
+ * uploads into caller-owned buffers and the caller broadcasts those buffers and the metadata blob; the
+ * other ranks import.  Replaces BwaIndex::build per process (bioseqdb/bwa.cpp:107-128). ---- */
+#define BSQ_N_TABLES 8   /* occ, occ32, sa, pac, ann_off, ann_id, ann_len, kmer (0 bytes = absent) */
+typedef struct { void *ptr; uint64_t bytes; } bsq_table;
+/* Bytes of each device table of a built index, and its metadata blob (meta == NULL: size query into
+ * *meta_bytes). */
+int bsq_index_layout(const bsq_index *idx, uint64_t *bytes, void *meta, uint64_t *meta_bytes);
+/* Like bsq_index_upload, into caller-owned device buffers (tables[i].bytes >= layout bytes[i]); the caller
+ * keeps them alive while the index is used. */
+int bsq_index_upload_into(bsq_index *idx, int device, const bsq_table *tables, int n_tables);
+/* A device-only index over caller-owned tables that hold an uploaded index's contents (e.g. received by a
+ * broadcast), described by its metadata blob.  Aligns and renders like the original. */
+int bsq_index_import(const void *meta, uint64_t meta_bytes, int device, const bsq_table *tables, int n_tables,
+                     bsq_index **out);
+
 /* ---- alignment --------------------------------------------------------------------------------- */
 /* Value of the (pos+1)-th lrand48() call of an unseeded glibc/musl process (Q10). */
 int64_t bsq_lrand48_at(uint64_t pos);
