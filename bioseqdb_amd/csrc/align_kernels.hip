@@ -672,9 +672,9 @@ struct EhRing {
 };
 
 template <class EH, class QA>
-DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
-                     int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
-                     int *_gscore, int *_max_off, EH eh, uint64_t &cells)
+DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                         int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
+                         int *_gscore, int *_max_off, EH eh, uint64_t &cells)
 {
     int i, j, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, beg, end, max, max_i, max_j, max_ins, max_del, max_ie,
         gscore, max_off;
@@ -714,24 +714,37 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, 
             hi = end;
         }
         cells += (uint64_t)(end > beg ? end - beg : 0);
-        for (j = beg; j < end; ++j) {
-            int2 p = eh.get(j);
-            int h, M = p.x, e = p.y;
-            p.x = h1;
-            M = M ? M + sc(tb, query(j)) : 0;
-            h = M > e ? M : e;
-            h = h > f ? h : f;
-            h1 = h;
-            mj = m > h ? mj : j;
-            m = m > h ? m : h;
-            t = M - oe_del; t = t > 0 ? t : 0;
-            e -= e_del; e = e > t ? e : t;
-            p.y = e;
-            eh.set(j, p);
-            t = M - oe_ins; t = t > 0 ? t : 0;
-            f -= e_ins; f = f > t ? f : t;
-        }
+        // The row reads column j+1 (eh and query) before it stores column j: the two never share a slot
+        // (the ring window is < 63 columns), so each cell's LDS round trip overlaps the previous cell's
+        // arithmetic.  The zero-trimming scans libbwa runs after the row (first non-zero column in
+        // [beg, end), last non-zero in [beg, end]) are tracked here from the values being stored; every
+        // stored h and e is >= 0, so "non-zero" is (h | e) != 0.
+        int nzf = beg < end ? end : beg, nzl = -1;   // (the serial scan's start values)
+        if (beg < end) {
+            int2 p = eh.get(beg);
+            int qj = query(beg);
+            for (j = beg; j < end; ++j) {
+                const int2 pn = eh.get(j + 1);
+                const int qn = j + 1 < end ? query(j + 1) : 0;
+                int h, M = p.x, e = p.y;
+                const int hx = h1;
+                M = M ? M + sc(tb, qj) : 0;
+                h = M > e ? M : e;
+                h = h > f ? h : f;
+                h1 = h;
+                mj = m > h ? mj : j;
+                m = m > h ? m : h;
+                t = M - oe_del; t = t > 0 ? t : 0;
+                e -= e_del; e = e > t ? e : t;
+                eh.set(j, make_int2(hx, e));
+                if ((hx | e) != 0) { nzl = j; nzf = nzf < j ? nzf : j; }
+                t = M - oe_ins; t = t > 0 ? t : 0;
+                f -= e_ins; f = f > t ? f : t;
+                p = pn; qj = qn;
+            }
+        } else j = beg;
         eh.set(end, make_int2(h1, 0));
+        if (h1 != 0) nzl = end;
         if (j == qlen) {
             max_ie = gscore > h1 ? max_ie : i;
             gscore = gscore > h1 ? gscore : h1;
@@ -748,9 +761,8 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, 
                 if (max - m - ((mj - max_j) - (i - max_i)) * e_ins > zdrop) break;
             }
         }
-        for (j = beg; j < end; ++j) { int2 v = eh.get(j); if (v.x != 0 || v.y != 0) break; }
-        beg = j;
-        for (j = end; j >= beg; --j) { int2 v = eh.get(j); if (v.x != 0 || v.y != 0) break; }
+        beg = nzf;
+        j = end < beg ? end : (nzl >= 0 ? nzl : beg - 1);
         end = j + 2 < qlen ? j + 2 : qlen;
     }
     *_qle = max_j + 1;
@@ -759,6 +771,16 @@ DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, 
     *_gscore = gscore;
     *_max_off = max_off;
     return max;
+}
+
+// global-memory variant (retry pass): an out-of-line call keeps the large-capacity kernel small
+template <class EH, class QA>
+DEVN int ksw_extend2(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                     int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
+                     int *_gscore, int *_max_off, EH eh, uint64_t &cells)
+{
+    return ksw_extend2_body(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, _qle,
+                            _tle, _gtle, _gscore, _max_off, eh, cells);
 }
 
 #define MINUS_INF (-0x40000000)
@@ -934,8 +956,16 @@ DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int 
                  int w, int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore, int *max_off,
                  EhSmall ehx, uint64_t &cells)
 {
-    return ksw_extend2(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, qle, tle, gtle,
-                       gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
+    // inlined: an out-of-line call spills the caller's live VGPRs to scratch around every extension
+    if (o.exp_flags & 8) {   // timing experiment: DP cycles land in the cell counter
+        const uint64_t t0 = clock64();
+        const int r = ksw_extend2_body(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0,
+                                       qle, tle, gtle, gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
+        cells += clock64() - t0;
+        return r;
+    }
+    return ksw_extend2_body(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, qle, tle,
+                            gtle, gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
 }
 template <class QA, class EH>
 DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins, int e_ins,
@@ -1208,6 +1238,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
     X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
     X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
+    const uint64_t t_k0 = clock64();
     for (int it = tid; it < n; it += nthr) {
         const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;
@@ -1232,12 +1263,15 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
             for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
         }
         if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
+        const uint64_t t1 = clock64();
         X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
         mark_primary_se(o, X, ids[r]);
         n_regs[li] = X.n;
+        if (o.exp_flags & 8) bases += clock64() - t1;   // timing experiment: dedup + primary cycles
     }
     wave_add(&ctr[STG_EXTEND].dp_cells, cells);
     wave_add(&ctr[STG_EXTEND].ref_bases, bases);
+    if (o.exp_flags & 8) wave_add(&ctr[STG_EXTEND].sa_values, clock64() - t_k0);   // timing experiment
 }
 
 // ------------------------------------------------------------------------------------------------

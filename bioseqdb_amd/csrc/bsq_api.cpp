@@ -1053,6 +1053,7 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
+        if (o.exp_flags & 8) b->stage_work[STG_CHAIN] = (double)c[STG_EXTEND].sa_values;   // timing experiment
     } else {
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
@@ -1199,6 +1200,7 @@ extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
         b->stage_bytes[STG_SMEM] =
             32.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
+        if (o.exp_flags & 8) b->stage_work[STG_CHAIN] = (double)c[STG_EXTEND].sa_values;   // timing experiment
     }
     b->seeded = true;
     return BSQ_OK;

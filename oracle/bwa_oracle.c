@@ -486,6 +486,16 @@ static void reverse_intvs(intv_v *p)
         }
 }
 
+#ifdef ORC_PROFILE
+/* seeding work profile (tools/seed_profile.py): bwt_extend calls by phase and by what the interval is
+ * (the string fits the GPU k-mer table / the interval has one occurrence / other) */
+uint64_t orc_prof[12];
+void orc_profile_get(uint64_t *out) { memcpy(out, orc_prof, sizeof orc_prof); }
+#define PROF(k) (++orc_prof[k])
+#else
+#define PROF(k) ((void)0)
+#endif
+
 /* bwt_smem1a with max_intv = 0 (as called through bwt_smem1) */
 static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int min_intv, intv_v *mem, intv_v *tmpv)
 {
@@ -503,6 +513,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
         if (ik.x[2] < max_intv) { VPUSH(*curr, ik); break; }
         else if (q[i] < 4) {
             c = 3 - q[i];
+            PROF(i - x + 1 <= 11 ? 0 : ik.x[2] == 1 ? 1 : 2);
             bwt_extend(b, &ik, ok, 0);
             if (ok[c].x[2] != ik.x[2]) {
                 VPUSH(*curr, ik);
@@ -517,9 +528,15 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
     swap = curr; curr = prev; prev = swap;
     for (i = x - 1; i >= -1; --i) {
         c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
+#ifdef ORC_PROFILE
+        if (prev->n == 1 && prev->a[0].x[2] == 1) PROF(9);
+#endif
         for (j = 0, curr->n = 0; j < (int)prev->n; ++j) {
             bwtintv_t *p = &prev->a[j];
-            if (c >= 0 && ik.x[2] >= max_intv) bwt_extend(b, p, ok, 1);
+            if (c >= 0 && ik.x[2] >= max_intv) {
+                PROF((int)(uint32_t)p->info - i <= 11 ? 3 : p->x[2] == 1 ? 4 : 5);
+                bwt_extend(b, p, ok, 1);
+            }
             if (c < 0 || ik.x[2] < max_intv || ok[c].x[2] < (uint64_t)min_intv) {
                 if (curr->n == 0) {
                     if (mem->n == 0 || (uint64_t)(i + 1) < mem->a[mem->n - 1].info >> 32) {
@@ -548,6 +565,7 @@ static int bwt_seed_strategy1(const orc_index *b, int len, const uint8_t *q, int
     for (i = x + 1; i < len; ++i) {
         if (q[i] < 4) {
             c = 3 - q[i];
+            PROF(i - x + 1 <= 11 ? 6 : ik.x[2] == 1 ? 7 : 8);
             bwt_extend(b, &ik, ok, 0);
             if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
                 *mem = ok[c];
