@@ -182,6 +182,8 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--index-build", default="device", choices=["device", "host"],
+                    help="where the index is built before the timed region (device: bsq_index_build_device)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
@@ -229,15 +231,19 @@ def main() -> int:
             L.bsq_free(p)
             ref_ns.append(buf)
             N.check(L.bsq_index_add_ref(idx, i + 1, ctypes.addressof(buf)))
-        hb.phase = "building the index on the host"
         t0 = time.time()
-        N.check(L.bsq_index_build(idx, 0))
+        if args.index_build == "device":   # suffix sort + BWT in HBM, leaves it uploaded
+            hb.phase = "building the index on the GPU"
+            N.check(L.bsq_index_build_device(idx, gpu))
+        else:
+            hb.phase = "building the index on the host"
+            N.check(L.bsq_index_build(idx, 0))
         t_build = time.time() - t0
     t0 = time.time()
     index_bufs = None
     if dist is None:
         hb.phase = "uploading the index"
-        N.check(L.bsq_index_upload(idx, gpu))
+        N.check(L.bsq_index_upload(idx, gpu))   # no-op for a device-built index
     else:   # one build, device tables broadcast to every rank (RCCL over xGMI)
         hb.phase = "replicating the index"
         from bioseqdb_amd import dist as D
@@ -357,6 +363,7 @@ def main() -> int:
         "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
         "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
         "index_build_s": round(t_build, 2),
+        "index_build": args.index_build,
         "index_upload_s": round(t_upload, 2),
         "retried_reads": retried,
     }
@@ -370,6 +377,7 @@ def main() -> int:
         for buf in ref_ns:
             oi.add_ref(len(oi._keep) + 1, bytes(buf.raw))
         eb = ctypes.c_int()
+        N.check(L.bsq_index_download(idx))   # host copy of the SA for the oracle's index
         sa = L.bsq_index_sa_data(idx, ctypes.byref(eb))
         oi.build_from_sa(sa, eb.value)
         oo = O.opts_from(opts)

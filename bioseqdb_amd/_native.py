@@ -105,6 +105,9 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                            ctypes.POINTER(ctypes.c_int64)]),
     "bsq_batch_retried": (ctypes.c_int64, [_P]),
+    "bsq_index_build_device": (ctypes.c_int, [_P, ctypes.c_int]),
+    "bsq_index_download": (ctypes.c_int, [_P]),
+    "bsq_index_build_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _lib = None

@@ -228,6 +228,12 @@ class BwaIndex:
         check(lib().bsq_index_build(self._h, threads))
         self._built = True
 
+    def build_on_device(self) -> None:
+        """BwaIndex::build on the GPU (suffix sort + BWT in HBM, SURVEY.md 8(f) row 1); leaves it uploaded."""
+        check(lib().bsq_index_build_device(self._h, self.device))
+        self._built = True
+        self._uploaded = True
+
     def upload(self) -> None:
         if not self._uploaded and self.l_pac > 0:
             check(lib().bsq_index_upload(self._h, self.device))

@@ -1397,6 +1397,8 @@ __global__ void k_pack(int n, SlotView mv, SlotView rv, const int32_t *retry_slo
         b.pad0 = 0;
         b.read_index = read_base + i;   // batch-wide read and CIGAR-arena positions
         b.cigar_off = (uint32_t)(cig_base + oc); b.n_cigar = (uint32_t)h.n_cigar;
+        static_assert(sizeof(bsq_hit) == 72, "bsq_hit layout");
+        reinterpret_cast<uint32_t *>(&b)[17] = 0;   // trailing padding: records are compared byte for byte
         const uint32_t *src = v.cigars + ((size_t)slot * v.cp.regs + g) * v.cp.cigar;
         for (int t = 0; t < h.n_cigar; ++t) out_cig[oc + t] = src[t];
         oc += h.n_cigar;

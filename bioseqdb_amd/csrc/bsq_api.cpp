@@ -54,6 +54,9 @@ hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Cap
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
+hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
+                           uint64_t *, int *, uint64_t *, std::string &);
+hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *);
 hipError_t launch_intv_counts(hipStream_t, int, const int32_t *, const uint32_t *, int64_t *);
 hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *, const uint32_t *, const int64_t *,
                             uint64_t *);
@@ -175,9 +178,12 @@ extern "C" int64_t bsq_index_seq_len(const bsq_index *idx) { return idx ? (int64
 extern "C" int64_t bsq_index_primary(const bsq_index *idx) { return idx ? (int64_t)idx->h.primary : -1; }
 extern "C" int32_t bsq_index_n_refs(const bsq_index *idx) { return idx ? (int32_t)idx->h.anns.size() : -1; }
 
+static bool host_tables(const HostIndex &h) { return !h.occ.empty(); }   // false: device-built, not downloaded
+
 extern "C" int64_t bsq_index_sa(const bsq_index *idx, int64_t row)
 {
     if (!idx || !idx->h.built || row < 0 || (uint64_t)row > idx->h.seq_len || idx->h.seq_len == 0) return -1;
+    if (!host_tables(idx->h)) return -1;
     return (int64_t)idx->h.sa((uint64_t)row);
 }
 
@@ -185,13 +191,14 @@ extern "C" int bsq_index_occ4(const bsq_index *idx, int64_t k, uint64_t cnt[4])
 {
     if (!idx || !idx->h.built || idx->h.seq_len == 0) { set_err("index not built"); return BSQ_E_INVALID; }
     if (k < -1 || (k >= 0 && (uint64_t)k > idx->h.seq_len)) { set_err("row out of range"); return BSQ_E_INVALID; }
+    if (!host_tables(idx->h)) { set_err("device-built index: call bsq_index_download first"); return BSQ_E_INVALID; }
     idx->h.occ4((uint64_t)k, cnt);
     return BSQ_OK;
 }
 
 extern "C" const void *bsq_index_sa_data(const bsq_index *idx, int *elem_bytes)
 {
-    if (!idx || !idx->h.built || idx->h.seq_len == 0) return nullptr;
+    if (!idx || !idx->h.built || idx->h.seq_len == 0 || !host_tables(idx->h)) return nullptr;
     if (!idx->h.sa32.empty()) { if (elem_bytes) *elem_bytes = 4; return idx->h.sa32.data(); }
     if (elem_bytes) *elem_bytes = 8;
     return idx->h.sa64.data();
@@ -221,14 +228,16 @@ static int kmer_depth(uint64_t seq_len)
 static void table_sizes(const HostIndex &h, uint64_t bytes[T_N], int &K, int &wide)
 {
     for (int t = 0; t < T_N; ++t) bytes[t] = 0;
-    wide = h.sa32.empty() ? 1 : 0;
+    const bool dev_only = h.dev_built && h.occ.empty();
+    wide = dev_only ? h.dev_wide : (h.sa32.empty() ? 1 : 0);
     const uint64_t nann = h.anns.size() ? h.anns.size() : 1;
     bytes[T_ANN_OFF] = nann * 8; bytes[T_ANN_ID] = nann * 8; bytes[T_ANN_LEN] = nann * 4;
     K = 0;
     if (h.seq_len == 0) return;
-    bytes[T_OCC] = h.occ.size() * sizeof(OccBlock);
-    bytes[T_OCC32] = wide ? 0 : h.occ.size() * 2 * sizeof(OccBlock32);
-    bytes[T_SA] = wide ? h.sa64.size() * 8 : h.sa32.size() * 4;
+    const uint64_t nblk = dev_only ? h.dev_nblk : h.occ.size();
+    bytes[T_OCC] = nblk * sizeof(OccBlock);
+    bytes[T_OCC32] = wide ? 0 : nblk * 2 * sizeof(OccBlock32);
+    bytes[T_SA] = (h.seq_len + 1) * (wide ? 8 : 4);
     bytes[T_PAC] = h.pac.size() + 16;
     K = kmer_depth(h.seq_len);
     bytes[T_KMER] = K ? (((uint64_t)1 << (2 * (K + 1))) - 4) / 3 * (wide ? 32 : 16) : 0;
@@ -268,11 +277,41 @@ static IndexMeta meta_of(const HostIndex &h)
     return m;
 }
 
+// A device-built index is already uploaded: bsq_index_upload on its device is a no-op, and
+// bsq_index_upload_into copies its tables into the caller's buffers (device to device) and adopts them.
+static int move_device_tables(bsq_index *idx, int device, const bsq_table *ext)
+{
+    HostIndex &h = idx->h;
+    DeviceIndex *d = h.dev;
+    if (device != d->device) { set_err("index was built on device %d", d->device); return BSQ_E_INVALID; }
+    if (!ext) return BSQ_OK;
+    HIPCHK(hipSetDevice(device));
+    const IndexMeta m = meta_of(h);
+    void *cur[T_N] = {d->occ, d->occ32, d->sa, d->pac, d->ann_off, d->ann_id, d->ann_len, d->kmer};
+    for (int t = 0; t < T_N; ++t) {
+        if (!m.table_bytes[t]) continue;
+        if (!ext[t].ptr || ext[t].bytes < m.table_bytes[t]) { set_err("table %d: buffer of %llu bytes, %llu needed", t,
+            (unsigned long long)ext[t].bytes, (unsigned long long)m.table_bytes[t]); return BSQ_E_INVALID; }
+        HIPCHK(hipMemcpy(ext[t].ptr, cur[t], m.table_bytes[t], hipMemcpyDeviceToDevice));
+    }
+    DeviceIndex *nd = new DeviceIndex();
+    nd->device = device;
+    nd->owned = false;
+    nd->occ = (OccBlock *)ext[T_OCC].ptr; nd->occ32 = (OccBlock32 *)ext[T_OCC32].ptr; nd->sa = ext[T_SA].ptr;
+    nd->pac = (uint8_t *)ext[T_PAC].ptr; nd->ann_off = (int64_t *)ext[T_ANN_OFF].ptr; nd->ann_id = (int64_t *)ext[T_ANN_ID].ptr;
+    nd->ann_len = (int32_t *)ext[T_ANN_LEN].ptr; nd->kmer = (uint32_t *)ext[T_KMER].ptr;
+    set_view(nd, m);
+    delete d;
+    h.dev = nd;
+    return BSQ_OK;
+}
+
 // Uploads the host index into its own allocations (ext == nullptr) or into caller-owned buffers.
 static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
 {
     if (!idx || !idx->h.built) { set_err("index not built"); return BSQ_E_INVALID; }
     const HostIndex &h = idx->h;
+    if (h.dev_built && h.dev) return move_device_tables(idx, device, ext);
     if (h.seq_len > 0 && h.occ.empty()) { set_err("device-only index (imported): nothing to upload from the host"); return BSQ_E_INVALID; }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
@@ -343,11 +382,118 @@ static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
 
 extern "C" int bsq_index_upload(bsq_index *idx, int device) { return upload_impl(idx, device, nullptr); }
 
+extern "C" int bsq_index_build_device(bsq_index *idx, int device)
+{
+    if (!idx) { set_err("null index"); return BSQ_E_INVALID; }
+    HostIndex &h = idx->h;
+    if (h.dev) { set_err("index already uploaded"); return BSQ_E_INVALID; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+        set_err("no HIP device %d (found %d); the index build has no CPU fallback here (bsq_index_build is the host path)",
+                device, ndev);
+        return BSQ_E_NODEV;
+    }
+    HIPCHK(hipSetDevice(device));
+    h.occ.clear(); h.sa32.clear(); h.sa64.clear();
+    h.l_pac = (int64_t)h.pac.size() * 4;
+    h.seq_len = (uint64_t)h.l_pac * 2;
+    h.primary = 0;
+    for (int c = 0; c < 5; ++c) h.L2[c] = 0;
+    const char *fw = getenv("BSQ_FORCE_WIDE");   // same row-width rule as the host build
+    h.dev_wide = (h.seq_len >= 0xFFFFFFFFull || (fw && *fw && *fw != '0')) ? 1 : 0;
+    h.dev_nblk = h.seq_len ? (h.seq_len + 127) / 128 + 1 : 0;
+    h.dev_built = true;
+    h.built = true;
+    const IndexMeta m = meta_of(h);
+    DeviceIndex *d = h.dev = new DeviceIndex();
+    d->device = device;
+    auto fail = [&](int rc) { delete h.dev; h.dev = nullptr; h.built = false; h.dev_built = false; return rc; };
+    void *ptr[T_N] = {};
+    for (int t : {(int)T_PAC, (int)T_ANN_OFF, (int)T_ANN_ID, (int)T_ANN_LEN, (int)T_OCC32, (int)T_KMER}) {
+        if (!m.table_bytes[t]) continue;
+        if (hipMalloc(&ptr[t], m.table_bytes[t]) != hipSuccess) { set_err("out of device memory (table %d)", t); return fail(BSQ_E_NOMEM); }
+    }
+    d->pac = (uint8_t *)ptr[T_PAC]; d->ann_off = (int64_t *)ptr[T_ANN_OFF]; d->ann_id = (int64_t *)ptr[T_ANN_ID];
+    d->ann_len = (int32_t *)ptr[T_ANN_LEN]; d->occ32 = (OccBlock32 *)ptr[T_OCC32]; d->kmer = (uint32_t *)ptr[T_KMER];
+    const size_t nann = h.anns.size() ? h.anns.size() : 1;
+    std::vector<int64_t> off(nann, 0), id(nann, 0);
+    std::vector<int32_t> len(nann, 0);
+    for (size_t i = 0; i < h.anns.size(); ++i) { off[i] = h.anns[i].offset; id[i] = h.anns[i].id; len[i] = h.anns[i].len; }
+    if (hipMemcpy(d->ann_off, off.data(), nann * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d->ann_id, id.data(), nann * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d->ann_len, len.data(), nann * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        set_err("uploading the annotations"); return fail(BSQ_E_HIP);
+    }
+    if (h.seq_len == 0) { set_view(d, m); return BSQ_OK; }
+    if (hipMemset(d->pac, 0, m.table_bytes[T_PAC]) != hipSuccess ||
+        hipMemcpy(d->pac, h.pac.data(), h.pac.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_err("uploading the pac"); return fail(BSQ_E_HIP);
+    }
+    std::string err;
+    int rounds = 0;
+    uint64_t tied = 0, nblk = 0, primary = 0, L2[5];
+    void *sa = nullptr;
+    OccBlock *occ = nullptr;
+    hipError_t e = gpu_build_index(d->pac, h.l_pac, h.dev_wide != 0, nullptr, &sa, &occ, &primary, L2, &nblk, &rounds,
+                                   &tied, err);
+    if (e != hipSuccess) {
+        set_err("GPU index build: %s", err.c_str());
+        return fail(e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? BSQ_E_NOMEM : BSQ_E_HIP);
+    }
+    d->sa = sa;
+    d->occ = occ;
+    h.primary = primary;
+    for (int c = 0; c < 5; ++c) h.L2[c] = L2[c];
+    h.dev_nblk = nblk;
+    h.dev_rounds = rounds;
+    h.dev_tied = tied;
+    const IndexMeta m2 = meta_of(h);
+    if (!m2.wide && launch_occ32(nullptr, d->occ, nblk, d->occ32) != hipSuccess) { set_err("occ32 build"); return fail(BSQ_E_HIP); }
+    IndexMeta mv = m2;
+    mv.kmer_k = 0;
+    set_view(d, mv);
+    if (m2.kmer_k > 0) {
+        d->view.kmer = d->kmer;
+        if (launch_kmer_build(nullptr, d->view, d->kmer, m2.kmer_k) != hipSuccess) { set_err("k-mer table build"); return fail(BSQ_E_HIP); }
+        d->view.kmer_k = m2.kmer_k;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) { set_err("GPU index build: %s", hipGetErrorString(hipGetLastError())); return fail(BSQ_E_HIP); }
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_build_stats(const bsq_index *idx, int *rounds, uint64_t *tied)
+{
+    if (!idx || !idx->h.dev_built) { set_err("not a device-built index"); return BSQ_E_INVALID; }
+    if (rounds) *rounds = idx->h.dev_rounds;
+    if (tied) *tied = idx->h.dev_tied;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_download(bsq_index *idx)
+{
+    if (!idx || !idx->h.built || !idx->h.dev) { set_err("index not on a device"); return BSQ_E_INVALID; }
+    HostIndex &h = idx->h;
+    if (!h.occ.empty() || h.seq_len == 0) return BSQ_OK;
+    HIPCHK(hipSetDevice(h.dev->device));
+    const IndexMeta m = meta_of(h);
+    try {
+        h.occ.resize(m.table_bytes[T_OCC] / sizeof(OccBlock));
+        if (m.wide) h.sa64.resize(h.seq_len + 1); else h.sa32.resize(h.seq_len + 1);
+    } catch (const std::bad_alloc &) {
+        h.occ.clear(); h.sa32.clear(); h.sa64.clear();
+        set_err("out of host memory"); return BSQ_E_NOMEM;
+    }
+    HIPCHK(hipMemcpy(h.occ.data(), h.dev->occ, m.table_bytes[T_OCC], hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(m.wide ? (void *)h.sa64.data() : (void *)h.sa32.data(), h.dev->sa, m.table_bytes[T_SA],
+                     hipMemcpyDeviceToHost));
+    return BSQ_OK;
+}
+
 extern "C" int bsq_index_layout(const bsq_index *idx, uint64_t *bytes, void *meta, uint64_t *meta_bytes)
 {
     if (!idx || !idx->h.built || !meta_bytes) { set_err("index not built / invalid argument"); return BSQ_E_INVALID; }
     const HostIndex &h = idx->h;
-    if (h.seq_len > 0 && h.occ.empty()) { set_err("device-only index (imported) has no host layout"); return BSQ_E_INVALID; }
+    if (h.seq_len > 0 && h.occ.empty() && !h.dev_built) { set_err("device-only index (imported) has no host layout"); return BSQ_E_INVALID; }
     const IndexMeta m = meta_of(h);
     if (bytes) for (int t = 0; t < T_N; ++t) bytes[t] = m.table_bytes[t];
     const uint64_t need = sizeof(IndexMeta) + h.anns.size() * sizeof(Ann) + h.holes.size() * sizeof(Hole);

@@ -53,6 +53,12 @@ struct HostIndex {
     std::vector<uint32_t> sa32;  // full SA of T$ when seq_len < 2^32
     std::vector<uint64_t> sa64;
     DeviceIndex *dev = nullptr;
+    // built on the device (bsq_index_build_device): SA and occ live only in HBM until bsq_index_download
+    bool dev_built = false;
+    int dev_wide = 0;
+    uint64_t dev_nblk = 0;
+    int dev_rounds = 0;        // prefix-doubling rounds after the first sort
+    uint64_t dev_tied = 0;     // suffixes still tied after the first (21-character) sort
 
     void add_ref(int64_t id, const uint8_t *ns);
     int build(int threads, std::string &err);

@@ -129,6 +129,7 @@ void HostIndex::occ4(uint64_t k, uint64_t c[4]) const
 int HostIndex::build(int threads, std::string &err)
 {
     built = false;
+    dev_built = false;
     occ.clear(); sa32.clear(); sa64.clear();
     if (pac.empty()) { built = true; l_pac = 0; seq_len = 0; return 0; }   // reference: index stays null
     if (threads < 1) threads = 1;

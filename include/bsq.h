@@ -97,8 +97,17 @@ void bsq_index_free(bsq_index *idx);
 int bsq_index_add_ref(bsq_index *idx, int64_t id, const void *nuclseq);
 /* Host build of T = pac || revcomp(pac), its suffix array, BWT, occ blocks.  `threads` <= 0: all cores. */
 int bsq_index_build(bsq_index *idx, int threads);
-/* Copies the built index into HBM of `device`. */
+/* Copies the built index into HBM of `device`.  No-op for an index built on that device. */
 int bsq_index_upload(bsq_index *idx, int device);
+/* GPU build (replaces BwaIndex::build, bioseqdb/bwa.cpp:107-128, and the
+ * host bsq_index_build + bsq_index_upload pair): suffix array of T$ by prefix doubling on rocPRIM radix
+ * sorts, BWT and occurrence blocks, all in HBM of `device`; the result is identical to the host build.
+ * Leaves the index uploaded; its SA and occ blocks stay on the device until bsq_index_download. */
+int bsq_index_build_device(bsq_index *idx, int device);
+/* Copies the SA and occ blocks of a device-built index to the host (bsq_index_sa / _occ4 / _sa_data). */
+int bsq_index_download(bsq_index *idx);
+/* Prefix-doubling rounds of the last device build and the suffixes still tied after its first sort. */
+int bsq_index_build_stats(const bsq_index *idx, int *rounds, uint64_t *tied);
 int64_t bsq_index_l_pac(const bsq_index *idx);
 int64_t bsq_index_seq_len(const bsq_index *idx);
 int64_t bsq_index_primary(const bsq_index *idx);

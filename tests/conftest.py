@@ -29,3 +29,16 @@ _ensure_built()
 def gpu_available():
     from bioseqdb_amd._native import lib
     return lib().bsq_device_count() > 0
+
+
+def pytest_sessionstart(session):
+    # Two HIP runtimes share this process: torch's bundled one and the system one libbsq links.  Both
+    # work when torch is loaded and has initialised the GPU before libbsq does (torch's HSA runtime is
+    # then the process-wide one); the other order leaves torch with "No HIP GPUs are available".  The
+    # multi-GPU driver orders them the same way (bench.py, bioseqdb_amd/dist.py).
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:   # counting does not initialise the GPU; init() does
+            torch.cuda.init()
+    except Exception:
+        pass

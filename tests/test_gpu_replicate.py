@@ -53,7 +53,19 @@ def test_import_matches_original(monkeypatch, wide):
         a = _align(L, pi.handle, pi.options, seqs, 17)
         b = _align(L, imp, pi.options, seqs, 17)
         assert len(a[0]) > 1000 * ctypes.sizeof(N.Hit)
-        assert a == b
+        if a != b:   # say which records differ
+            import numpy as np
+            ha = np.frombuffer(a[0], np.uint8).reshape(-1, ctypes.sizeof(N.Hit))
+            hb = np.frombuffer(b[0], np.uint8).reshape(-1, ctypes.sizeof(N.Hit))
+            diff = np.where((ha != hb).any(1))[0] if ha.shape == hb.shape else None
+            ex = ""
+            if diff is not None and len(diff):
+                k = int(diff[0])
+                ra = N.Hit.from_buffer_copy(a[0][k * ctypes.sizeof(N.Hit):(k + 1) * ctypes.sizeof(N.Hit)])
+                rb = N.Hit.from_buffer_copy(b[0][k * ctypes.sizeof(N.Hit):(k + 1) * ctypes.sizeof(N.Hit)])
+                ex = {f: (getattr(ra, f), getattr(rb, f)) for f, _ in N.Hit._fields_ if getattr(ra, f) != getattr(rb, f)}
+            raise AssertionError(f"{ex} hits {ha.shape} vs {hb.shape}, differing {None if diff is None else (len(diff), diff[:8].tolist())}, "
+                                 f"cigar equal {a[1] == b[1]}, offsets equal {a[2] == b[2]}")
     finally:
         L.bsq_index_free(imp)
         del src, dst
