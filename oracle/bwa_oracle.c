@@ -440,10 +440,24 @@ void orc_index_occ4(const orc_index *idx, int64_t k, uint64_t cnt[4]) { bwt_occ4
 
 typedef struct { uint64_t x[3], info; } bwtintv_t;
 
+/* SURVEY.md section 8(d) algorithmic bytes, counted on libbwa's own layout (the figure behind the bench's
+ * roofline `achieved`): [0] 64 B per occ block a bwt_extend touches (bwt_2occ4: one block when both
+ * ranks share a 128-base interval, else two; a rank of -1 reads nothing), [1] 8 B per bwt_sa value,
+ * [2] ceil(bases/4) per reference window of the extension (bns_fetch_seq), [3] the same for the windows
+ * of CIGAR generation and patching (bns_get_seq).  Per thread, summed per batch (orc_algo_bytes). */
+static __thread uint64_t orc_ab[4];
+static uint64_t orc_ab_last[4];
+void orc_algo_bytes(uint64_t out[4]) { memcpy(out, orc_ab_last, sizeof orc_ab_last); }
+
 /* bwt_extend (bwt_2occ4 yields exactly two bwt_occ4 results) */
 static void bwt_extend(const orc_index *b, const bwtintv_t *ik, bwtintv_t ok[4], int is_back)
 {
     uint64_t tk[4], tl[4];
+    {
+        const uint64_t k = ik->x[!is_back] - 1, l = k + ik->x[2];
+        const uint64_t kk = k - (k >= b->primary), ll = l - (l >= b->primary);
+        orc_ab[0] += k == (uint64_t)-1 || (kk >> 7) == (ll >> 7) ? 64 : 128;
+    }
     bwt_occ4(b, ik->x[!is_back] - 1, tk);
     bwt_occ4(b, ik->x[!is_back] - 1 + ik->x[2], tl);
     for (int i = 0; i != 4; ++i) {
@@ -466,6 +480,7 @@ static inline uint64_t bwt_invPsi(const orc_index *b, uint64_t k)
 
 static uint64_t bwt_sa(const orc_index *b, uint64_t k)
 {
+    orc_ab[1] += 8;
     uint64_t sa = 0, mask = (uint64_t)b->sa_intv - 1;
     while (k & mask) { ++sa; k = bwt_invPsi(b, k); }
     return sa + b->sa[k / b->sa_intv];
@@ -652,6 +667,7 @@ static uint8_t *bns_get_seq(int64_t l_pac, const uint8_t *pac, int64_t beg, int6
     if (beg >= l_pac || end <= l_pac) {
         int64_t k, l = 0;
         *len = end - beg;
+        orc_ab[3] += (uint64_t)((end - beg + 3) >> 2);
         seq = malloc(end - beg > 0 ? (size_t)(end - beg) : 1);
         if (beg >= l_pac) {
             int64_t beg_f = (l_pac << 1) - 1 - end, end_f = (l_pac << 1) - 1 - beg;
@@ -673,7 +689,11 @@ static uint8_t *bns_fetch_seq(const orc_index *x, int64_t *beg, int64_t mid, int
     if (is_rev) { int64_t t = far_beg; far_beg = (x->l_pac << 1) - far_end; far_end = (x->l_pac << 1) - t; }
     *beg = *beg > far_beg ? *beg : far_beg;
     *end = *end < far_end ? *end : far_end;
-    return bns_get_seq(x->l_pac, x->pac.a, *beg, *end, &len);
+    const uint64_t before = orc_ab[3];
+    uint8_t *seq = bns_get_seq(x->l_pac, x->pac.a, *beg, *end, &len);
+    orc_ab[2] += orc_ab[3] - before;   /* an extension window, not a CIGAR one */
+    orc_ab[3] = before;
+    return seq;
 }
 
 /* ============================================================================================== */
@@ -1698,7 +1718,7 @@ int64_t orc_lrand48_at(uint64_t pos)
 /* ---- batch (bench cpu_baseline) ------------------------------------------------------------- */
 typedef struct {
     const orc_index *idx; const mopt_t *opt; const uint8_t *codes; const int64_t *off;
-    int lo, hi; uint64_t first_call; int64_t nreg; uint64_t ck; int err;
+    int lo, hi; uint64_t first_call; int64_t nreg; uint64_t ck; int err; uint64_t ab[4];
 } job_t;
 
 static inline uint64_t fnv(uint64_t h, uint64_t v) { for (int i = 0; i < 8; ++i) { h ^= (v >> (8 * i)) & 0xff; h *= 0x100000001b3ULL; } return h; }
@@ -1708,6 +1728,7 @@ static void *batch_worker(void *arg)
     job_t *j = arg;
     alnreg_v regs = {0, 0, 0};
     uint64_t ck = 0;
+    memset(orc_ab, 0, sizeof orc_ab);
     for (int r = j->lo; r < j->hi; ++r) {
         int len = (int)(j->off[r + 1] - j->off[r]);
         const uint8_t *q = j->codes + j->off[r];
@@ -1726,6 +1747,7 @@ static void *batch_worker(void *arg)
         j->nreg += (int64_t)regs.n;
     }
     j->ck = ck;
+    memcpy(j->ab, orc_ab, sizeof orc_ab);
     free(regs.a);
     return NULL;
 }
@@ -1736,6 +1758,7 @@ static void *seed_worker(void *arg)
     job_t *j = arg;
     intv_v mem = {0, 0, 0}, mem1 = {0, 0, 0}, tmpv[2] = {{0, 0, 0}, {0, 0, 0}};
     uint64_t ck = 0;
+    memset(orc_ab, 0, sizeof orc_ab);
     for (int r = j->lo; r < j->hi; ++r) {
         int len = (int)(j->off[r + 1] - j->off[r]);
         mem_collect_intv(j->opt, j->idx, len, j->codes + j->off[r], &mem, &mem1, tmpv);
@@ -1748,6 +1771,7 @@ static void *seed_worker(void *arg)
         j->nreg += (int64_t)mem.n;
     }
     j->ck = ck;
+    memcpy(j->ab, orc_ab, sizeof orc_ab);
     free(mem.a); free(mem1.a); free(tmpv[0].a); free(tmpv[1].a);
     return NULL;
 }
@@ -1762,11 +1786,15 @@ int64_t orc_seed_batch(const orc_index *idx, const orc_opts *o, const uint8_t *c
     job_t *jobs = calloc((size_t)threads, sizeof(job_t));
     for (int t = 0; t < threads; ++t) {
         jobs[t] = (job_t){ idx, &opt, codes, offsets, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads),
-                           0, 0, 0, 0 };
+                           0, 0, 0, 0, {0, 0, 0, 0} };
         pthread_create(&th[t], NULL, seed_worker, &jobs[t]);
     }
     int64_t nint = 0; uint64_t ck = 0;
-    for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); nint += jobs[t].nreg; ck += jobs[t].ck; }
+    memset(orc_ab_last, 0, sizeof orc_ab_last);
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL); nint += jobs[t].nreg; ck += jobs[t].ck;
+        for (int c = 0; c < 4; ++c) orc_ab_last[c] += jobs[t].ab[c];
+    }
     free(th); free(jobs);
     if (checksum) *checksum = ck;
     return nint;
@@ -1782,11 +1810,15 @@ int64_t orc_align_batch(const orc_index *idx, const orc_opts *o, const uint8_t *
     job_t *jobs = calloc((size_t)threads, sizeof(job_t));
     for (int t = 0; t < threads; ++t) {
         jobs[t] = (job_t){ idx, &opt, codes, offsets, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads),
-                           first_call, 0, 0, 0 };
+                           first_call, 0, 0, 0, {0, 0, 0, 0} };
         pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
     }
     int64_t nreg = 0; uint64_t ck = 0; int err = 0;
-    for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); nreg += jobs[t].nreg; ck += jobs[t].ck; err |= jobs[t].err; }
+    memset(orc_ab_last, 0, sizeof orc_ab_last);
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL); nreg += jobs[t].nreg; ck += jobs[t].ck; err |= jobs[t].err;
+        for (int c = 0; c < 4; ++c) orc_ab_last[c] += jobs[t].ab[c];
+    }
     free(th); free(jobs);
     if (checksum) *checksum = ck;
     return err ? -1 : nreg;

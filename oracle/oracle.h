@@ -100,6 +100,11 @@ int64_t orc_seed_batch(const orc_index *idx, const orc_opts *opt, const uint8_t 
 int64_t orc_align_batch(const orc_index *idx, const orc_opts *opt, const uint8_t *codes, const int64_t *offsets,
                         int n, uint64_t first_call, int threads, uint64_t *checksum);
 
+/* SURVEY.md 8(d) algorithmic bytes of the last orc_seed_batch / orc_align_batch, on libbwa's layout:
+ * [0] occ blocks of bwt_extend x 64 B, [1] bwt_sa values x 8 B, [2] extension reference windows
+ * ceil(bases/4) (bns_fetch_seq), [3] CIGAR / patch windows ceil(bases/4) (bns_get_seq). */
+void orc_algo_bytes(uint64_t out[4]);
+
 /* ksw restatements exposed for brute-force tests. */
 int orc_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat,
                     int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0,
