@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbsq.so")
+LIB_PATH = os.environ.get("BSQ_LIB") or os.path.join(_HERE, "libbsq.so")   # BSQ_LIB: experiment builds only
 
 BSQ_OK = 0
 BSQ_E_INVALID = -1
