@@ -896,6 +896,164 @@ DEV int gen_cigar2(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, i
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_flt_seeds: mem_flt_chained_seeds (bwamem.c) for reads long enough to trigger it (5.5 ln l <= 0.05 l,
+// l >~ 700): seeds shorter than MEM_SHORT_LEN whose +-50-base neighbourhood scores below the HSP
+// threshold under ksw_align2 (mem_seed_sw) leave their chain; kept seeds take that score (len*a when no
+// SW ran), which orders them in mem_chain2aln.  Shorter reads keep score = len and skip all of this.
+// ------------------------------------------------------------------------------------------------
+#define KSW_P 8
+DEV int sub0(int a, int b) { return a > b ? a - b : 0; }   // _mm_subs_epu16 on values >= 0
+
+// r.score of ksw_align2(..., KSW_XSTART) -> ksw_i16: a lane-for-lane emulation of the striped SSE2 kernel
+// (see oracle/bwa_oracle.c ksw_align2_score for why the striping shows in the result).  buf: 3*slen*8 int16.
+DEV int ksw_i16_score(const Score sc, int qlen, const uint8_t *query, int tlen, const DIndex &ix, int64_t tbeg,
+                      int o_del, int e_del, int o_ins, int e_ins, int16_t *buf, uint64_t &cells)
+{
+    const int slen = (qlen + KSW_P - 1) / KSW_P, oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    int16_t *H0 = buf, *H1 = buf + slen * KSW_P, *E = buf + 2 * slen * KSW_P;
+    for (int j = 0; j < slen * KSW_P; ++j) { H0[j] = 0; E[j] = 0; }
+    int gmax = 0;
+    for (int i = 0; i < tlen; ++i) {
+        int f[KSW_P], mx[KSW_P], h[KSW_P];
+        const int tb = ref_at(ix, tbeg + i);
+        h[0] = 0;
+#pragma unroll
+        for (int k = 0; k < KSW_P; ++k) { f[k] = 0; mx[k] = 0; if (k) h[k] = H0[(slen - 1) * KSW_P + k - 1]; }
+        for (int j = 0; j < slen; ++j) {
+#pragma unroll
+            for (int k = 0; k < KSW_P; ++k) {
+                const int pos = j + k * slen;
+                int v = h[k] + (pos < qlen ? sc(tb, query[pos]) : 0);
+                const int e = E[j * KSW_P + k];
+                v = v > e ? v : e;
+                v = v > f[k] ? v : f[k];
+                mx[k] = mx[k] > v ? mx[k] : v;
+                H1[j * KSW_P + k] = (int16_t)v;
+                const int en = sub0(e, e_del), t = sub0(v, oe_del);
+                E[j * KSW_P + k] = (int16_t)(en > t ? en : t);
+                const int fn = sub0(f[k], e_ins), t2 = sub0(v, oe_ins);
+                f[k] = fn > t2 ? fn : t2;
+                h[k] = H0[j * KSW_P + k];
+            }
+        }
+        cells += (uint64_t)slen * KSW_P;
+        for (int kk = 0; kk < 16; ++kk) {   // lazy F: into H only, at most 16 sweeps
+#pragma unroll
+            for (int k = KSW_P - 1; k > 0; --k) f[k] = f[k - 1];
+            f[0] = 0;
+            bool more = true;
+            for (int j = 0; j < slen && more; ++j) {
+                more = false;
+#pragma unroll
+                for (int k = 0; k < KSW_P; ++k) {
+                    int v = H1[j * KSW_P + k];
+                    v = v > f[k] ? v : f[k];
+                    H1[j * KSW_P + k] = (int16_t)v;
+                    const int hv = sub0(v, oe_ins);
+                    f[k] = sub0(f[k], e_ins);
+                    more |= f[k] > hv;
+                }
+            }
+            if (!more) break;
+        }
+        int imax = 0;
+#pragma unroll
+        for (int k = 0; k < KSW_P; ++k) imax = imax > mx[k] ? imax : mx[k];
+        gmax = gmax > imax ? gmax : imax;
+        int16_t *sw = H0; H0 = H1; H1 = sw;
+    }
+    return gmax;
+}
+
+// mem_seed_sw: -1 when the seed needs no SW
+DEV int mem_seed_sw(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const Seed &sd, int16_t *buf,
+                    uint64_t &cells, uint64_t &bases)
+{
+    const int64_t l_pac = ix.l_pac;
+    if (sd.len >= 200) return -1;
+    int qb = sd.qbeg, qe = sd.qbeg + sd.len;
+    int64_t rb = sd.rbeg, re = sd.rbeg + sd.len;
+    const int64_t mid = (rb + re) >> 1;
+    qb -= 50; qb = qb > 0 ? qb : 0;
+    qe += 50; qe = qe < l_query ? qe : l_query;
+    rb -= 50; rb = rb > 0 ? rb : 0;
+    re += 50; re = re < l_pac << 1 ? re : l_pac << 1;
+    if (rb < l_pac && l_pac < re) {
+        if (mid < l_pac) re = l_pac;
+        else rb = l_pac;
+    }
+    if (qe - qb >= 200 || re - rb >= 200) return -1;
+    {   // bns_fetch_seq: clamp to the row (strand-flipped) containing mid
+        int is_rev;
+        const int rid = pos2rid(ix, depos(ix, mid, is_rev));
+        int64_t far_beg = ix.ann_off[rid], far_end = far_beg + ix.ann_len[rid];
+        if (is_rev) { const int64_t t = far_beg; far_beg = (l_pac << 1) - far_end; far_end = (l_pac << 1) - t; }
+        rb = rb > far_beg ? rb : far_beg;
+        re = re < far_end ? re : far_end;
+    }
+    if (re <= rb) return 0;
+    bases += (uint64_t)((re - rb + 3) >> 2);
+    return ksw_i16_score(score_of(o), qe - qb, q + qb, (int)(re - rb), ix, rb, o.o_del, o.e_del, o.o_ins, o.e_ins, buf,
+                         cells);
+}
+
+__global__ void __launch_bounds__(256) k_flt_seeds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
+                                                   const int64_t *offs, const int32_t *sel, int n, ChainDesc *chains,
+                                                   Seed *seeds, const int32_t *n_chains, const uint32_t *status,
+                                                   int32_t *sscore, uint8_t *scratch, Counters *ctr)
+{
+    const int nthr = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    int16_t *buf = reinterpret_cast<int16_t *>(scratch + (size_t)tid * cp.scratch);
+    uint64_t cells = 0, bases = 0;
+    for (int li = tid; li < n; li += nthr) {
+        if (status[li]) continue;
+        const int r = read_of(sel, li);
+        const int len = (int)(offs[r + 1] - offs[r]);
+        const uint8_t *q = codes + offs[r];
+        // the float/double mix of bwamem.c: MEM_MINSC_COEF 5.5f * log(), MEM_SEEDSW_COEF 0.05f * l_query
+        const double min_l = o.min_chain_weight ? 1.1f * o.min_chain_weight : 5.5f * log((double)len);
+        const bool active = !(min_l > (double)(0.05f * (float)len));
+        const int min_hsp = (int)(o.a * min_l + .499);
+        ChainDesc *cd = chains + (size_t)li * cp.chains;
+        Seed *sd = seeds + (size_t)li * cp.seeds;
+        int32_t *ss = sscore + (size_t)li * cp.seeds;
+        const int nc = n_chains[li];
+        for (int c = 0; c < nc; ++c) {
+            Seed *cs = sd + cd[c].seed_off;
+            int32_t *cscore = ss + cd[c].seed_off;
+            int k = 0;
+            for (int j = 0; j < cd[c].n; ++j) {
+                const Seed t = cs[j];
+                int score = t.len;   // mem_chain: s.score = s.len
+                if (active) {
+                    score = mem_seed_sw(ix, o, len, q, t, buf, cells, bases);
+                    if (!(score < 0 || score >= min_hsp)) continue;
+                    score = score < 0 ? t.len * o.a : score;
+                }
+                cs[k] = t;
+                cscore[k] = score;
+                ++k;
+            }
+            cd[c].n = k;
+        }
+    }
+    wave_add(&ctr[STG_CHAIN].dp_cells, cells);
+    wave_add(&ctr[STG_CHAIN].ref_bases, bases);
+}
+
+hipError_t launch_flt_seeds(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp,
+                            const uint8_t *codes, const int64_t *offs, const int32_t *sel, int n, ChainDesc *chains,
+                            Seed *seeds, const int32_t *n_chains, const uint32_t *status, int32_t *sscore,
+                            uint8_t *scratch, Counters *ctr)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_flt_seeds, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, n, chains, seeds, n_chains,
+                       status, sscore, scratch, ctr);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_extend: mem_chain2aln for every chain, mem_sort_dedup_patch, mem_mark_primary_se
 // ------------------------------------------------------------------------------------------------
 DEV int cal_max_gap(const DOpts &o, int qlen)
@@ -978,7 +1136,7 @@ DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int 
 
 template <class EH, class QM>
 DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
-                   ExtCtx &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
+                   const int32_t *sscore, ExtCtx &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
 {
     int64_t l_pac = ix.l_pac, rmax0, rmax1;
     if (c.n == 0) return;
@@ -1006,7 +1164,8 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
         bases += (uint64_t)((rmax1 - rmax0 + 3) >> 2);
     }
     uint64_t *srt = X.srt;
-    for (int i = 0; i < c.n; ++i) srt[i] = (uint64_t)(uint32_t)seeds[i].len << 32 | (uint64_t)i;   // score == len
+    // seed score: len (mem_chain), or mem_flt_chained_seeds' score for long reads
+    for (int i = 0; i < c.n; ++i) srt[i] = (uint64_t)(uint32_t)(sscore ? sscore[i] : seeds[i].len) << 32 | (uint64_t)i;
     for (int i = 1; i < c.n; ++i) {   // keys are unique: any correct sort equals ks_introsort_64
         uint64_t t = srt[i];
         int j = i;
@@ -1227,7 +1386,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
                                                            int n, const ChainDesc *chains, const Seed *seeds,
                                                            const int32_t *n_chains, Reg *regs_out, int32_t *n_regs,
                                                            uint32_t *status, uint8_t *scratch, Counters *ctr,
-                                                           const int32_t *order)
+                                                           const int32_t *order, const int32_t *sscore)
 {
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1250,17 +1409,20 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
         X.n = 0; X.cap = cp.regs; X.ovf = false;
         const ChainDesc *cd = chains + (size_t)li * cp.chains;
         const Seed *sd = seeds + (size_t)li * cp.seeds;
+        const int32_t *ss = sscore ? sscore + (size_t)li * cp.seeds : nullptr;
         const int nc = n_chains[li];
         if (LDS) {
             EhSmall ehx{(int)threadIdx.x, &X.ovf};   // blockDim == 64: lane-interleaved LDS columns
             const int qoff = 64 * EXT_LDS_COLS * 4 + (int)threadIdx.x;
             for (int j = 0; j < len; ++j) g_lds_q8[qoff + j * 64] = q[j];   // stage the read in LDS
             QMakeL qm{qoff};
-            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
+            for (int c = 0; c < nc && !X.ovf; ++c)
+                chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
         } else {
             EhG ehx{X.eh};
             QMakeG qm{q};
-            for (int c = 0; c < nc && !X.ovf; ++c) chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, X, ehx, qm, cells, bases);
+            for (int c = 0; c < nc && !X.ovf; ++c)
+                chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
         }
         if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
         const uint64_t t1 = clock64();
@@ -1515,7 +1677,7 @@ hipError_t launch_ext_key(hipStream_t st, const Caps &cp, const int64_t *offs, c
 hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                          const int64_t *offs, const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
                          const Seed *seeds, const int32_t *n_chains, Reg *regs, int32_t *n_regs, uint32_t *status,
-                         uint8_t *scratch, Counters *ctr, const int32_t *order)
+                         uint8_t *scratch, Counters *ctr, const int32_t *order, const int32_t *sscore)
 {
     // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
     static const bool force_g = getenv("BSQ_EXT") && getenv("BSQ_EXT")[0] == 'g';   // timing experiments only
@@ -1525,10 +1687,10 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
         static const size_t sh_env = getenv("BSQ_EXT_SH") ? (size_t)atol(getenv("BSQ_EXT_SH")) : 0;   // tuning only
         const size_t sh = std::max((size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2), sh_env);
         hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
-                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order);
+                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
     } else {
         hipLaunchKernelGGL(k_extend<false>, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds,
-                           n_chains, regs, n_regs, status, scratch, ctr, order);
+                           n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
     }
     return hipGetLastError();
 }

@@ -30,7 +30,10 @@ hipError_t launch_chain(int, hipStream_t, const DIndex &, const DOpts &, const C
                         Counters *);
 hipError_t launch_extend(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                          const int32_t *, const int64_t *, int, const ChainDesc *, const Seed *, const int32_t *, Reg *,
-                         int32_t *, uint32_t *, uint8_t *, Counters *, const int32_t *);
+                         int32_t *, uint32_t *, uint8_t *, Counters *, const int32_t *, const int32_t *);
+hipError_t launch_flt_seeds(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
+                            const int32_t *, int, ChainDesc *, Seed *, const int32_t *, const uint32_t *, int32_t *,
+                            uint8_t *, Counters *);
 hipError_t launch_ext_key(hipStream_t, const Caps &, const int64_t *, const int32_t *, int, const ChainDesc *,
                           const Seed *, const int32_t *, const uint32_t *, uint32_t *, int32_t *);
 hipError_t launch_reg2aln(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
@@ -613,6 +616,7 @@ struct Workspace {
     uint32_t *cigars = nullptr;
     uint8_t *scratch = nullptr;
     int32_t *sel = nullptr;   // local slot -> read (retry workspace only)
+    int32_t *sscore = nullptr; // seed scores of mem_flt_chained_seeds (long-read workspaces only)
     uint8_t *zslab = nullptr; // per-wave traceback spill slabs of the wave reg2aln kernel
     int64_t zslab_bytes = 0;
     int zslab_blocks = 0;
@@ -627,11 +631,20 @@ struct Workspace {
     {
         hipFree(status); hipFree(intv); hipFree(n_intv); hipFree(n_chains); hipFree(n_regs); hipFree(n_cig);
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
+        hipFree(sscore);
         hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
         hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill);
         *this = Workspace{};
     }
 };
+
+// mem_flt_chained_seeds is active for a read of length l when !(5.5f*ln(l) > 0.05f*l) (bwamem.c), i.e.
+// l >= ~700; a workspace for such lengths carries seed scores and runs k_flt_seeds
+bool long_reads(int max_len)
+{
+    if (max_len < 2) return false;
+    return !(5.5f * std::log((double)max_len) > (double)(0.05f * (float)max_len));
+}
 
 int64_t scratch_bytes(const Caps &c, int64_t z_cap)
 {
@@ -668,8 +681,10 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     w.scratch_total = (int64_t)w.grid * 256 * w.cp.scratch;
     HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
     if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
+    if (long_reads(cp.max_len)) HIPCHK(hipMalloc(&w.sscore, R * cp.seeds * 4));
     if (!with_sel) {
-        w.zslab_bytes = (int64_t)(2 * cp.max_len + 8) * (int64_t)(2 * cp.max_len + 64);
+        // (bands of long reads that need more go to the retry pass, whose per-thread scratch holds 4 MB)
+        w.zslab_bytes = std::min<int64_t>((int64_t)(2 * cp.max_len + 8) * (int64_t)(2 * cp.max_len + 64), 4 << 20);
         w.zslab_blocks = (int)std::min<int64_t>(((int64_t)R + 3) / 4, 3 * 256);
         HIPCHK(hipMalloc(&w.zslab, (size_t)w.zslab_blocks * 4 * (size_t)w.zslab_bytes));
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
@@ -734,6 +749,7 @@ struct bsq_batch {
     // seeding-only runs (bsq_batch_seed): main-pass intervals stay in the workspace slots, reads that
     // needed the retry kernel keep theirs here; bsq_batch_intervals packs both on demand
     int32_t chunk = 0;   // reads per workspace pass; larger batches run in chunks [lo, lo + chunk)
+    int32_t chunk0 = 0;  // the pass size for short reads (BSQ_CHUNK or 1M)
     int32_t lo = 0;      // first read of the chunk being run (stage kernels see offs + lo, ids + lo)
     bool seeded = false, seed_packed = false;
     std::vector<std::pair<int32_t, std::vector<uint64_t>>> seed_retry;
@@ -807,7 +823,7 @@ extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_b
     {   // workspace pass size (BSQ_CHUNK overrides; tests use it to exercise multi-chunk batches)
         const char *e = getenv("BSQ_CHUNK");
         const int c = e && atoi(e) > 0 ? atoi(e) : (1 << 20);
-        b->chunk = std::max(1, std::min(std::max(max_reads, 1), c));
+        b->chunk = b->chunk0 = std::max(1, std::min(std::max(max_reads, 1), c));
     }
     *out = b;
     HIPCHK(hipSetDevice(b->device));
@@ -871,9 +887,13 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
         HIPCHK(hipMemcpyAsync(b->codes, b->h_codes.data(), (size_t)total, hipMemcpyHostToDevice, b->stream));
         HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (size_t)(n_reads + 1) * 8, hipMemcpyHostToDevice, b->stream));
     }
-    // (re)allocate the main workspace for this read length
-    if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1)) {
+    // (re)allocate the main workspace for this read length; the per-read slots grow with the length, so
+    // long reads run in proportionally smaller workspace passes (~ the bytes of 1M x 150 bp)
+    const int32_t want = max_len > 150 ? std::max<int32_t>(1, std::min<int64_t>(b->chunk0, (int64_t)b->chunk0 * 150 / max_len))
+                                       : b->chunk0;
+    if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1) || want != b->chunk) {
         b->main.release();
+        b->chunk = want;
         int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device), 32 * 1024, false);
         if (rc) return rc;
     }
@@ -917,6 +937,9 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
     HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
                         w.scratch, b->ctr));
+    if (w.sscore)   // long reads: mem_flt_chained_seeds (per read; shorter reads of the batch keep score = len)
+        HIPCHK(launch_flt_seeds(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.chains, w.seeds,
+                                w.n_chains, w.status, w.sscore, w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
     const int32_t *order = nullptr;
     static const bool no_sort = getenv("BSQ_EXT_SORT") && getenv("BSQ_EXT_SORT")[0] == '0';
@@ -928,7 +951,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         order = w.eidx1;
     }
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,
-                         w.n_regs, w.status, w.scratch, b->ctr, order));
+                         w.n_regs, w.status, w.scratch, b->ctr, order, w.sscore));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
     if (!sel && w.cp.max_len <= 1024) {
         // main pass: one wave per read, DP rows across lanes, eh + traceback in LDS (dp_wave.hip)
@@ -1160,10 +1183,6 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len <= 0) {
         set_err("gap extension penalties, max_occ and min_seed_len must be positive");
         return BSQ_E_INVALID;
-    }
-    if (b->max_len >= 700) {   // mem_flt_chained_seeds becomes active: not implemented on this path yet
-        double l = b->max_len;
-        if (!(5.5 * std::log(l) > 0.05 * l)) { set_err("reads of %d bp need mem_flt_chained_seeds (unsupported)", b->max_len); return BSQ_E_UNSUPPORTED; }
     }
     HIPCHK(hipSetDevice(b->device));
     const int n = b->n_reads;

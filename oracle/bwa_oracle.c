@@ -1512,22 +1512,136 @@ static void mem_mark_primary_se(const mopt_t *opt, int n, mem_alnreg_t *a, int64
     free(z.a);
 }
 
-/* mem_align1 (no mem_flt_chained_seeds effect for reads with 5.5*ln(l) > 0.05*l, i.e. l < ~700) */
+/* ksw_align2(..., KSW_XSTART, 0) as mem_seed_sw uses it (ksw.c: ksw_qinit with size 2 -> ksw_i16); only
+ * r.score is read.  Restated as a scalar emulation of the striped SSE2 kernel, lane for lane, because its
+ * result is not the plain Gotoh optimum: p = 8 int16 lanes, query position j + k*slen in lane k of vector
+ * j (slen = ceil(qlen/8), padding scores 0).  Per target row: the main loop computes H = max(diag + s, E,
+ * F) with F carried only within a lane's segment, records the row maximum and updates E from that H; the
+ * "lazy F" loop (at most 16 sweeps, leaving as soon as no lane has f > H - oe_ins) then carries F across
+ * segment boundaries into H only -- neither E nor the maximum see those corrections.  Gap terms saturate
+ * at 0 (_mm_subs_epu16); the score is the best row maximum (KSW_XSTOP unset: no early stop). */
+#define KSW_P 8
+static inline int sub0(int a, int b) { return a > b ? a - b : 0; }   /* _mm_subs_epu16 on values >= 0 */
+static int ksw_align2_score(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat,
+                            int o_del, int e_del, int o_ins, int e_ins)
+{
+    const int slen = (qlen + KSW_P - 1) / KSW_P, oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    int16_t *H0 = calloc((size_t)slen * KSW_P, 2), *H1 = calloc((size_t)slen * KSW_P, 2), *E = calloc((size_t)slen * KSW_P, 2);
+    int gmax = 0;
+    for (int i = 0; i < tlen; ++i) {
+        int f[KSW_P] = {0}, mx[KSW_P] = {0}, h[KSW_P];
+        const int8_t *ma = mat + target[i] * 5;
+        h[0] = 0;
+        for (int k = 1; k < KSW_P; ++k) h[k] = H0[(slen - 1) * KSW_P + k - 1];
+        for (int j = 0; j < slen; ++j) {
+            for (int k = 0; k < KSW_P; ++k) {
+                const int pos = j + k * slen;
+                int v = h[k] + (pos < qlen ? ma[query[pos]] : 0);
+                const int e = E[j * KSW_P + k];
+                v = v > e ? v : e;
+                v = v > f[k] ? v : f[k];
+                mx[k] = mx[k] > v ? mx[k] : v;
+                H1[j * KSW_P + k] = (int16_t)v;
+                const int en = sub0(e, e_del), t = sub0(v, oe_del);
+                E[j * KSW_P + k] = (int16_t)(en > t ? en : t);
+                const int fn = sub0(f[k], e_ins), t2 = sub0(v, oe_ins);
+                f[k] = fn > t2 ? fn : t2;
+                h[k] = H0[j * KSW_P + k];
+            }
+        }
+        for (int kk = 0; kk < 16; ++kk) {
+            for (int k = KSW_P - 1; k > 0; --k) f[k] = f[k - 1];
+            f[0] = 0;
+            int more = 1;
+            for (int j = 0; j < slen && more; ++j) {
+                more = 0;
+                for (int k = 0; k < KSW_P; ++k) {
+                    int v = H1[j * KSW_P + k];
+                    v = v > f[k] ? v : f[k];
+                    H1[j * KSW_P + k] = (int16_t)v;
+                    const int hv = sub0(v, oe_ins);
+                    f[k] = sub0(f[k], e_ins);
+                    if (f[k] > hv) more = 1;
+                }
+            }
+            if (!more) break;
+        }
+        int imax = 0;
+        for (int k = 0; k < KSW_P; ++k) imax = imax > mx[k] ? imax : mx[k];
+        if (imax > gmax) gmax = imax;
+        int16_t *sw = H0; H0 = H1; H1 = sw;
+    }
+    free(H0); free(H1); free(E);
+    return gmax;
+}
+
+#define MEM_SHORT_EXT 50
+#define MEM_SHORT_LEN 200
+#define MEM_HSP_COEF 1.1f
+#define MEM_MINSC_COEF 5.5f
+#define MEM_SEEDSW_COEF 0.05f
+
+/* mem_seed_sw (bwamem.c): SW score of a short seed's neighbourhood, -1 when no SW is needed */
+static int mem_seed_sw(const mopt_t *opt, const orc_index *bns, int l_query, const uint8_t *query, const mem_seed_t *s)
+{
+    int qb, qe, rid;
+    int64_t rb, re, mid, l_pac = bns->l_pac;
+    if (s->len >= MEM_SHORT_LEN) return -1;
+    qb = s->qbeg, qe = s->qbeg + s->len;
+    rb = s->rbeg, re = s->rbeg + s->len;
+    mid = (rb + re) >> 1;
+    qb -= MEM_SHORT_EXT; qb = qb > 0 ? qb : 0;
+    qe += MEM_SHORT_EXT; qe = qe < l_query ? qe : l_query;
+    rb -= MEM_SHORT_EXT; rb = rb > 0 ? rb : 0;
+    re += MEM_SHORT_EXT; re = re < l_pac << 1 ? re : l_pac << 1;
+    if (rb < l_pac && l_pac < re) {
+        if (mid < l_pac) re = l_pac;
+        else rb = l_pac;
+    }
+    if (qe - qb >= MEM_SHORT_LEN || re - rb >= MEM_SHORT_LEN) return -1;
+    uint8_t *rseq = bns_fetch_seq(bns, &rb, mid, &re, &rid);
+    const int sc = ksw_align2_score(qe - qb, query + qb, (int)(re - rb), rseq, opt->mat, opt->o_del, opt->e_del,
+                                    opt->o_ins, opt->e_ins);
+    free(rseq);
+    return sc;
+}
+
+/* mem_flt_chained_seeds (bwamem.c): for reads long enough, seeds whose neighbourhood scores below the
+ * HSP threshold are dropped and the kept ones take the SW score (or len*a when no SW was run) */
+static void mem_flt_chained_seeds(const mopt_t *opt, const orc_index *bns, int l_query, const uint8_t *query, int n_chn,
+                                  mem_chain_t *a)
+{
+    double min_l = opt->min_chain_weight ? MEM_HSP_COEF * opt->min_chain_weight : MEM_MINSC_COEF * log(l_query);
+    int i, j, k, min_HSP_score = (int)(opt->a * min_l + .499);
+    if (min_l > MEM_SEEDSW_COEF * l_query) return;
+    for (i = 0; i < n_chn; ++i) {
+        mem_chain_t *c = &a[i];
+        for (j = k = 0; j < c->n; ++j) {
+            mem_seed_t *s = &c->seeds[j];
+            s->score = mem_seed_sw(opt, bns, l_query, query, s);
+            if (s->score < 0 || s->score >= min_HSP_score) {
+                s->score = s->score < 0 ? s->len * opt->a : s->score;
+                c->seeds[k++] = *s;
+            }
+        }
+        c->n = k;
+    }
+}
+
+int orc_ksw_align2_score(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat, int o_del,
+                         int e_del, int o_ins, int e_ins)
+{
+    return ksw_align2_score(qlen, query, tlen, target, mat, o_del, e_del, o_ins, e_ins);
+}
+
+/* mem_align1 = mem_align1_core + mem_mark_primary_se (bwamem.c) */
 static int mem_align1(const mopt_t *opt, const orc_index *idx, int l_seq, const uint8_t *seq, int64_t id, alnreg_v *regs)
 {
     chain_v chn = {0, 0, 0};
     regs->n = 0;
     mem_chain(opt, idx, l_seq, seq, &chn);
     chn.n = (size_t)mem_chain_flt(opt, (int)chn.n, chn.a);
-    {   /* mem_flt_chained_seeds guard */
-        double min_l = opt->min_chain_weight ? 1.1 * opt->min_chain_weight : 5.5 * log(l_seq);
-        if (!(min_l > 0.05 * l_seq) && chn.n > 0) {
-            fprintf(stderr, "[oracle] reads long enough to trigger mem_flt_chained_seeds are not supported\n");
-            for (size_t i = 0; i < chn.n; ++i) free(chn.a[i].seeds);
-            free(chn.a);
-            return -1;
-        }
-    }
+    mem_flt_chained_seeds(opt, idx, l_seq, seq, (int)chn.n, chn.a);
     for (size_t i = 0; i < chn.n; ++i) {
         mem_chain2aln(opt, idx, l_seq, seq, &chn.a[i], regs);
         free(chn.a[i].seeds);

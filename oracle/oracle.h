@@ -106,6 +106,9 @@ int64_t orc_align_batch(const orc_index *idx, const orc_opts *opt, const uint8_t
 void orc_algo_bytes(uint64_t out[4]);
 
 /* ksw restatements exposed for brute-force tests. */
+/* r.score of ksw_align2(..., KSW_XSTART) (striped ksw_i16 emulated lane for lane; mem_seed_sw). */
+int orc_ksw_align2_score(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat, int o_del,
+                         int e_del, int o_ins, int e_ins);
 int orc_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat,
                     int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0,
                     int *qle, int *tle, int *gtle, int *gscore, int *max_off);

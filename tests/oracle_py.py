@@ -67,6 +67,7 @@ def lib() -> ctypes.CDLL:
             "orc_align_batch": (ctypes.c_int64, [P, ctypes.POINTER(OrcOpts), P, P, ctypes.c_int, ctypes.c_uint64,
                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
             "orc_algo_bytes": (None, [ctypes.POINTER(ctypes.c_uint64)]),
+            "orc_ksw_align2_score": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P] + [ctypes.c_int] * 4),
             "orc_ksw_extend2": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P] + [ctypes.c_int] * 8 +
                                 [ctypes.POINTER(ctypes.c_int)] * 5),
             "orc_ksw_global2": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P] + [ctypes.c_int] * 5 +

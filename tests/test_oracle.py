@@ -307,3 +307,57 @@ def test_planted_reads():
     m = align(clip)[0]
     assert m.cigar.endswith("110M") and m.cigar.startswith("40N") and m.query_match_begin == 40   # Q8: clip prints N
     assert align("ACGT" * 4) == []                                  # shorter than min_seed_len
+
+
+# ---- ksw_align2 score (mem_seed_sw, the long-read seed filter) -------------------------------------------
+def _mat(a=1, b=4):
+    mat = []
+    for i in range(5):
+        for j in range(5):
+            mat.append(-1 if i == 4 or j == 4 else (a if i == j else -b))
+    return (ctypes.c_int8 * 25)(*mat)
+
+
+def _gotoh_local(q, t, mat, od, ed, oi, ei):
+    """Plain affine-gap Smith-Waterman (E: deletion along the target, F: insertion along the query)."""
+    best = 0
+    H = [0] * (len(q) + 1)
+    E = [0] * (len(q) + 1)
+    for i in range(len(t)):
+        diag, f = 0, 0
+        newH = [0] * (len(q) + 1)
+        for j in range(len(q)):
+            h = max(diag + mat[t[i] * 5 + q[j]], E[j], f, 0)
+            diag = H[j]
+            newH[j] = h
+            best = max(best, h)
+            E[j] = max(E[j] - ed, h - od - ed, 0)
+            f = max(f - ei, h - oi - ei, 0)
+        H = newH
+    return best
+
+
+def _ksw(q, t, mat, od=6, ed=6, oi=1, ei=1):
+    qa, ta = bytes(q), bytes(t)
+    return O.lib().orc_ksw_align2_score(len(q), qa, len(t), ta, mat, od, ed, oi, ei)
+
+
+def test_ksw_align2_score_identity_and_bounds():
+    import random
+    mat = _mat()
+    r = random.Random(11)
+    for n in (1, 7, 8, 9, 31, 64, 150, 199):
+        s = [r.randrange(4) for _ in range(n)]
+        assert _ksw(s, s, mat) == n
+    for _ in range(60):
+        q = [r.randrange(4) for _ in range(r.randrange(5, 90))]
+        t = [r.randrange(4) for _ in range(r.randrange(5, 90))]
+        if r.random() < 0.5:   # related pair with an insertion and mismatches
+            t = q[: len(q) // 2] + q[len(q) // 2 + 3:]
+            t = [x if r.random() > 0.05 else (x + 1) % 4 for x in t]
+        g = _gotoh_local(q, t, list(mat), 6, 6, 1, 1)
+        k = _ksw(q, t, mat)
+        assert 0 <= k <= g   # the striped kernel's lazy F never raises the maximum or E
+        # without insertions (a prohibitive open penalty) F never fires: the striped result is the optimum
+        assert _ksw(q, t, mat, oi=1000) == _gotoh_local(q, t, list(mat), 6, 6, 1000, 1)
+
