@@ -169,6 +169,48 @@ def gpu_checksum(hits: "N.Hits", n_reads: int) -> int:
     return ck
 
 
+def reads_as_nuclseq(L, reads):
+    """nuclseq varlenas of the batch's reads (sequence.h:18-38), for the host rendering measurement: the
+    reads without N packed in numpy (padding bases as nuclseq_from_text draws them), the rest through
+    bsq_nuclseq_from_text.  Returns (buffers to keep alive, ctypes array of pointers)."""
+    n = reads.n
+    lens = np.diff(reads.offsets)
+    ptrs = (ctypes.c_void_p * max(n, 1))()
+    keep = []
+    L0 = int(lens[0]) if n else 0
+    plain = np.zeros(n, dtype=bool)
+    if n and L0 and (lens == L0).all():
+        codes = reads.codes.reshape(n, L0)
+        plain = (codes < 4).all(axis=1)
+        nb = (L0 + 3) // 4
+        pad = np.zeros((n, nb * 4), dtype=np.uint8)
+        pad[:, :L0] = codes
+        x = L0 % 2147483647 or 1   # std::minstd_rand(holes_num ^ len) with no holes
+        for j in range(L0, nb * 4):
+            x = x * 48271 % 2147483647
+            pad[:, j] = x & 3
+        q = pad.reshape(n, nb, 4).astype(np.uint8)
+        pac = (q[:, :, 0] << 6 | q[:, :, 1] << 4 | q[:, :, 2] << 2 | q[:, :, 3]).astype(np.uint8)
+        size = 12 + nb
+        buf = np.zeros((n, size), dtype=np.uint8)
+        buf[:, 0:4] = np.frombuffer(np.uint32(size << 2).tobytes(), np.uint8)
+        buf[:, 8:12] = np.frombuffer(np.uint32(L0).tobytes(), np.uint8)
+        buf[:, 12:] = pac
+        keep.append(buf)
+        base = buf.ctypes.data
+        for i in np.nonzero(plain)[0]:
+            ptrs[int(i)] = base + int(i) * size
+    for i in np.nonzero(~plain)[0]:
+        t = reads.text(int(i)).encode()
+        size = ctypes.c_size_t()
+        p = L.bsq_nuclseq_from_text(t, len(t), ctypes.byref(size))
+        b = ctypes.create_string_buffer(ctypes.string_at(p, size.value), size.value)
+        L.bsq_free(p)
+        keep.append(b)
+        ptrs[int(i)] = ctypes.addressof(b)
+    return keep, ptrs
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,6 +409,27 @@ def main() -> int:
         "index_upload_s": round(t_upload, 2),
         "retried_reads": retried,
     }
+
+    # ---- host materialisation: the last step's rows rendered as bwa_result text ----
+    if rank == 0 and not cfg["seeding"] and n_hits:
+        hb.phase = "rendering rows on the host"
+        keep, ptrs = reads_as_nuclseq(L, reads)
+        t1 = time.perf_counter()
+        p = L.bsq_render_tsv(idx, L.bsq_batch_hits(batch), ptrs)
+        dt_r = time.perf_counter() - t1
+        nbytes = len(ctypes.string_at(p)) if p else 0
+        L.bsq_free(p)
+        os.environ["BSQ_RENDER_THREADS"] = "1"   # the reference's single-backend rendering, for comparison
+        t1 = time.perf_counter()
+        L.bsq_free(L.bsq_render_tsv(idx, L.bsq_batch_hits(batch), ptrs))
+        dt_1 = time.perf_counter() - t1
+        del os.environ["BSQ_RENDER_THREADS"]
+        result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
+                                 "rows_per_s_1thread": round(n_hits / dt_1, 1),
+                                 "text_MB": round(nbytes / 1e6, 1), "threads": min(16, os.cpu_count() or 1),
+                                 "note": "bsq_render_tsv of the last step (BwaMatch text, Q3/Q7/Q8 rules); "
+                                         "outside the timed region"}
+        del keep, ptrs
 
     # ---- CPU baseline: the oracle on this host, bounded sample, rank 0 at N = 1 only ----
     hb.phase = "CPU baseline"

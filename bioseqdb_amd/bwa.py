@@ -15,6 +15,10 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import hashlib
+import os
+import struct
+from collections import OrderedDict
 from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
 
 from . import _native
@@ -213,7 +217,10 @@ class BwaIndex:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            lib().bsq_index_free(h)
+            try:
+                lib().bsq_index_free(h)
+            except Exception:   # interpreter shutdown (cached indexes): the process releases everything
+                pass
             self._h = None
 
     @property
@@ -296,15 +303,60 @@ def _iterate_nuclseq_table(rows: Iterable[Row]) -> Iterator[Tuple[int, Nucleotid
         yield rid, seq
 
 
+class _IndexCache:
+    """Cross-call index cache: the reference rebuilds the index from
+    ``reference_sql`` on every call (extension.cpp:326,359); here an index is keyed by a digest of its
+    rows (ids and nuclseq bytes, in cursor order) and the device, so repeated calls over the same
+    reference skip the build and the upload.  Options are per call and are not part of the key.
+    ``BSQ_INDEX_CACHE`` = number of indexes kept (default 2, 0 disables)."""
+
+    def __init__(self):
+        self._d: "OrderedDict[tuple, BwaIndex]" = OrderedDict()
+        self.hits = 0
+        self.builds = 0
+
+    @staticmethod
+    def capacity() -> int:
+        return max(0, int(os.environ.get("BSQ_INDEX_CACHE", "2")))
+
+    def get(self, rows: List[Tuple[int, NucleotideSequence]], device: int) -> BwaIndex:
+        h = hashlib.blake2b(digest_size=20)
+        for rid, seq in rows:
+            h.update(struct.pack("<qQ", rid, len(seq.raw)))
+            h.update(seq.raw)
+        key = (h.digest(), len(rows), device)
+        cap = self.capacity()
+        if cap and key in self._d:
+            self._d.move_to_end(key)
+            self.hits += 1
+            return self._d[key]
+        idx = BwaIndex(device)
+        for rid, seq in rows:
+            idx.add_ref_sequence(rid, seq)
+        if rows and lib().bsq_device_count() > device:
+            idx.build_on_device()   # suffix sort + BWT in HBM (bsq_index_build_device)
+        else:
+            idx.build()             # same tables from the host build (alignment itself needs the GPU)
+        self.builds += 1
+        if cap:
+            self._d[key] = idx
+            while len(self._d) > cap:
+                self._d.popitem(last=False)
+        return idx
+
+    def clear(self) -> None:
+        self._d.clear()
+        self.hits = self.builds = 0
+
+
+INDEX_CACHE = _IndexCache()
+
+
 def bwa_index_from_query(reference_rows: Iterable[Row], opts: Optional[BwaOptions], device: int = 0) -> BwaIndex:
-    """bwa_index_from_query (extension.cpp:211-236)."""
-    idx = BwaIndex(device)
-    count = 0
-    for rid, seq in _iterate_nuclseq_table(reference_rows):
-        idx.add_ref_sequence(rid, seq)
-        count += 1
-    idx.options = effective_opts(opts, count)
-    idx.build()
+    """bwa_index_from_query (extension.cpp:211-236), through the cross-call cache."""
+    rows = list(_iterate_nuclseq_table(reference_rows))
+    idx = INDEX_CACHE.get(rows, device)
+    idx.options = effective_opts(opts, len(rows))
     return idx
 
 

@@ -1,67 +1,161 @@
 // render.cpp -- bwa_result row rendering (reference: BwaIndex::align_sequence's BwaMatch fields,
 // bioseqdb/bwa.cpp:198-226, extract_reference_subseq :104-117, cigar_compressed_to_string :119-126,
 // and the htslib bam_cigar_opchr table "MIDNSHP=XB", so libbwa's clip op 3 prints as 'N' -- Q8).
+//
+// Host materialisation: once alignment runs on the GPU, rendering the rows is the
+// host's share of every cursor batch, so it runs on all host cores (reads split by hit count, one text
+// buffer per thread, concatenated in read order), looks holes up by offset instead of scanning every
+// hole for every row, and formats integers without temporaries.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/bsq.h"
 #include "bsq_index.h"
 
 using namespace bsq;
 
+namespace {
 
-static std::string ref_subseq(const HostIndex &h, int64_t rb, int64_t re)
+struct HoleRef { int64_t beg, end; uint32_t order; char amb; };
+
+// Holes ordered by offset, with the longest length: the holes overlapping [rb, re) are those with
+// offset in (rb - max_len, re).  Overlapping holes (Q3: offsets of different rows share one axis) are
+// applied in their original order, as the reference's loop does.
+struct HoleIndex {
+    std::vector<HoleRef> by_off;
+    int64_t max_len = 0;
+    explicit HoleIndex(const std::vector<Hole> &holes)
+    {
+        by_off.reserve(holes.size());
+        for (size_t i = 0; i < holes.size(); ++i) {
+            by_off.push_back(HoleRef{holes[i].offset, holes[i].offset + holes[i].len, (uint32_t)i, holes[i].amb});
+            max_len = std::max<int64_t>(max_len, holes[i].len);
+        }
+        std::sort(by_off.begin(), by_off.end(), [](const HoleRef &a, const HoleRef &b) { return a.beg < b.beg; });
+    }
+};
+
+void ref_subseq(const HostIndex &h, const HoleIndex &hx, int64_t rb, int64_t re, std::string &out)
 {
-    std::string s((size_t)(re - rb), '?');
+    const size_t base = out.size();
+    out.resize(base + (size_t)(re - rb));
+    char *s = &out[base];
     if (rb < h.l_pac) {
-        for (int64_t i = 0; i < re - rb; ++i) s[(size_t)i] = "ACGT"[pac_get(h.pac.data(), (uint64_t)(rb + i))];
-        for (const Hole &hl : h.holes) {   // Q3: hole offsets are row-relative but compared as concatenated
-            int64_t lo = std::max<int64_t>(hl.offset, rb), hi = std::min<int64_t>(hl.offset + hl.len, re);
-            for (int64_t i = lo; i < hi; ++i) s[(size_t)(i - rb)] = hl.amb;
+        for (int64_t i = 0; i < re - rb; ++i) s[i] = "ACGT"[pac_get(h.pac.data(), (uint64_t)(rb + i))];
+        if (hx.by_off.empty()) return;
+        const int64_t lo_off = rb - hx.max_len;
+        auto it = std::lower_bound(hx.by_off.begin(), hx.by_off.end(), lo_off,
+                                   [](const HoleRef &a, int64_t v) { return a.beg < v; });
+        HoleRef hit[64];
+        int nh = 0;
+        std::vector<HoleRef> many;
+        for (; it != hx.by_off.end() && it->beg < re; ++it) {
+            if (it->end <= rb) continue;
+            if (nh < 64) hit[nh++] = *it; else many.push_back(*it);
+        }
+        if (!many.empty()) many.insert(many.begin(), hit, hit + nh);
+        HoleRef *v = many.empty() ? hit : many.data();
+        const size_t n = many.empty() ? (size_t)nh : many.size();
+        std::sort(v, v + n, [](const HoleRef &a, const HoleRef &b) { return a.order < b.order; });
+        for (size_t k = 0; k < n; ++k) {
+            const int64_t lo = std::max<int64_t>(v[k].beg, rb), hi = std::min<int64_t>(v[k].end, re);
+            for (int64_t i = lo; i < hi; ++i) s[i - rb] = v[k].amb;
         }
     } else {
         // Q7: the reference reads past the forward pac here (undefined behaviour); render the
         // reverse-strand reference text instead.
         for (int64_t i = 0; i < re - rb; ++i)
-            s[(size_t)i] = "ACGT"[3 - pac_get(h.pac.data(), (uint64_t)((h.l_pac << 1) - 1 - (rb + i)))];
+            s[i] = "ACGT"[3 - pac_get(h.pac.data(), (uint64_t)((h.l_pac << 1) - 1 - (rb + i)))];
     }
-    return s;
 }
 
-extern "C" char *bsq_render_tsv(const bsq_index *idx, const bsq_hits *hits, const void *const *reads)
+inline void put_int(std::string &out, int64_t v)
 {
-    if (!idx || !hits) return nullptr;
-    std::string out;
-    for (int32_t r = 0; r < hits->n_reads; ++r) {
-        int64_t b = hits->read_off[r], e = hits->read_off[r + 1];
+    char buf[24];
+    int n = 0;
+    const bool neg = v < 0;
+    uint64_t u = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    do { buf[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    if (neg) buf[n++] = '-';
+    while (n) out += buf[--n];
+}
+
+void render_reads(const HostIndex &h, const HoleIndex &hx, const bsq_hits *hits, const void *const *reads, int32_t r0,
+                  int32_t r1, std::string &out)
+{
+    std::string text;
+    for (int32_t r = r0; r < r1; ++r) {
+        const int64_t b = hits->read_off[r], e = hits->read_off[r + 1];
         if (b == e) continue;
-        std::string text = ns_to_text(static_cast<const uint8_t *>(reads[r]));
+        text = ns_to_text(static_cast<const uint8_t *>(reads[r]));
         for (int64_t k = b; k < e; ++k) {
             const bsq_hit &x = hits->hits[k];
-            out += std::to_string(x.ref_id); out += '\t';
-            out += ref_subseq(idx->h, x.rb, x.re); out += '\t';
-            out += std::to_string(x.ref_match_start); out += '\t';
-            out += std::to_string(x.ref_match_end); out += '\t';
-            out += std::to_string(x.ref_match_len); out += '\t';
+            put_int(out, x.ref_id); out += '\t';
+            ref_subseq(h, hx, x.rb, x.re, out); out += '\t';
+            put_int(out, x.ref_match_start); out += '\t';
+            put_int(out, x.ref_match_end); out += '\t';
+            put_int(out, x.ref_match_len); out += '\t';
             out.append(text, (size_t)x.qb, (size_t)(x.qe - x.qb)); out += '\t';
-            out += std::to_string(x.qb); out += '\t';
-            out += std::to_string(x.qe); out += '\t';
-            out += std::to_string(x.qe - x.qb); out += '\t';
+            put_int(out, x.qb); out += '\t';
+            put_int(out, x.qe); out += '\t';
+            put_int(out, x.qe - x.qb); out += '\t';
             out += x.is_primary ? 't' : 'f'; out += '\t';
             out += x.is_secondary ? 't' : 'f'; out += '\t';
             out += x.is_reverse ? 't' : 'f'; out += '\t';
             for (uint32_t c = 0; c < x.n_cigar; ++c) {
-                uint32_t v = hits->cigar[x.cigar_off + c];
-                out += std::to_string(v >> 4);
+                const uint32_t v = hits->cigar[x.cigar_off + c];
+                put_int(out, v >> 4);
                 out += "MIDNSHP=XB"[v & 0xf];
             }
             out += '\t';
-            out += std::to_string(x.score);
+            put_int(out, x.score);
             out += '\n';
         }
     }
-    char *s = (char *)malloc(out.size() + 1);
-    memcpy(s, out.c_str(), out.size() + 1);
+}
+
+int render_threads(int64_t n_hits)
+{
+    const char *e = getenv("BSQ_RENDER_THREADS");
+    int t = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    t = std::max(1, std::min(t, 16));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(t, n_hits / 2048 + 1));   // small batches: one thread
+}
+
+}  // namespace
+
+extern "C" char *bsq_render_tsv(const bsq_index *idx, const bsq_hits *hits, const void *const *reads)
+{
+    if (!idx || !hits) return nullptr;
+    const HoleIndex hx(idx->h.holes);
+    const int32_t n = hits->n_reads;
+    const int T = n > 0 ? render_threads(hits->n_hits) : 1;
+    std::vector<std::string> part((size_t)T);
+    std::vector<int32_t> cut((size_t)T + 1, n);
+    cut[0] = 0;
+    for (int t = 1; t < T; ++t) {   // equal numbers of rows per thread
+        const int64_t target = hits->n_hits * t / T;
+        cut[t] = (int32_t)(std::lower_bound(hits->read_off, hits->read_off + n, target) - hits->read_off);
+        cut[t] = std::max(cut[t], cut[t - 1]);
+    }
+    auto work = [&](int t) {
+        part[t].reserve((size_t)((hits->n_hits / T + 1) * 400));
+        render_reads(idx->h, hx, hits, reads, cut[t], cut[t + 1], part[t]);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    size_t total = 0;
+    for (auto &p : part) total += p.size();
+    char *s = (char *)malloc(total + 1);
+    if (!s) return nullptr;
+    size_t o = 0;
+    for (auto &p : part) { memcpy(s + o, p.data(), p.size()); o += p.size(); }
+    s[o] = 0;
     return s;
 }

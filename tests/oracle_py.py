@@ -114,7 +114,10 @@ class OracleIndex:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_index_free(self.h)
+            try:
+                lib().orc_index_free(self.h)
+            except Exception:   # interpreter shutdown
+                pass
             self.h = None
 
     def add_ref(self, ref_id: int, raw: bytes) -> None:

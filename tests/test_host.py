@@ -50,3 +50,19 @@ def test_empty_reference_returns_no_rows_and_no_lrand48_call():
 
 def test_result_columns():
     assert B.BWA_RESULT_COLUMNS[5] == "query_id" and len(B.BWA_RESULT_COLUMNS) == 15
+
+
+def test_index_cache_across_calls(monkeypatch):
+    # the same reference rows reuse one index; different rows build anew
+    monkeypatch.setenv("BSQ_INDEX_CACHE", "2")
+    B.INDEX_CACHE.clear()
+    r1 = [(1, NucleotideSequence.from_text("ACGTTGCA" * 50)), (2, NucleotideSequence.from_text("GGCCA" * 40))]
+    r2 = [(1, NucleotideSequence.from_text("ACGTTGCA" * 50)), (3, NucleotideSequence.from_text("GGCCA" * 40))]
+    a = B.bwa_index_from_query(r1, None)
+    b = B.bwa_index_from_query(list(r1) + [(None, None)], bwa_opts(max_occ=7))   # NULL rows do not change the key
+    assert a is b and b.options.max_occ == 7
+    c = B.bwa_index_from_query(r2, None)   # another id: another index
+    assert c is not a and B.INDEX_CACHE.builds == 2 and B.INDEX_CACHE.hits == 1
+    monkeypatch.setenv("BSQ_INDEX_CACHE", "0")
+    assert B.bwa_index_from_query(r1, None) is not a
+    B.INDEX_CACHE.clear()
