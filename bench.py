@@ -424,6 +424,14 @@ def main() -> int:
         L.bsq_free(L.bsq_render_tsv(idx, L.bsq_batch_hits(batch), ptrs))
         dt_1 = time.perf_counter() - t1
         del os.environ["BSQ_RENDER_THREADS"]
+        tt, tn = ctypes.c_void_p(), ctypes.c_int64()
+        N.check(L.bsq_batch_render(batch, ptrs, ctypes.byref(tt), ctypes.byref(tn)))   # warm (buffers)
+        t1 = time.perf_counter()
+        N.check(L.bsq_batch_render(batch, ptrs, ctypes.byref(tt), ctypes.byref(tn)))
+        dt_g = time.perf_counter() - t1
+        result["gpu_render"] = {"rows": n_hits, "seconds": round(dt_g, 4), "rows_per_s": round(n_hits / dt_g, 1),
+                                "text_MB": round(tn.value / 1e6, 1), "same_bytes_as_host": int(tn.value) == nbytes,
+                                "note": "bsq_batch_render: rows rendered on the GPU incl. record upload and text D2H"}
         result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
                                  "rows_per_s_1thread": round(n_hits / dt_1, 1),
                                  "text_MB": round(nbytes / 1e6, 1), "threads": min(16, os.cpu_count() or 1),

@@ -57,6 +57,14 @@ hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Cap
 hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
+struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
+struct RenderView {
+    const bsq_hit *hits; const uint32_t *cigar; int64_t n_hits; const uint8_t *pac; int64_t l_pac;
+    const RenderHole *holes; int32_t n_holes; int64_t hole_max; const uint8_t *codes; const int64_t *offs;
+    const int64_t *rh_off; const RenderHole *rh;
+};
+hipError_t launch_row_len(hipStream_t, const RenderView &, int64_t *);
+hipError_t launch_row_write(hipStream_t, const RenderView &, const int64_t *, char *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
 hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *);
@@ -765,6 +773,11 @@ struct bsq_batch {
     std::vector<uint32_t> res_cig;
     std::vector<int64_t> res_off;
     bsq_hits view{};
+    // GPU rendering (bsq_batch_render): device copies of the records, row lengths/offsets, text
+    bsq_hit *r_hits = nullptr; uint32_t *r_cig = nullptr; int64_t *r_len = nullptr; char *r_text = nullptr;
+    int64_t r_hits_cap = 0, r_cig_cap = 0, r_len_cap = 0, r_text_cap = 0;
+    char *r_host = nullptr; int64_t r_host_cap = 0;
+    void *r_tmp = nullptr; size_t r_tmp_bytes = 0;
     hipEvent_t ev[STG_N + 1]{};
     float stage_ms[STG_N]{};
     double stage_bytes[STG_N]{};
@@ -859,6 +872,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->cnt_hits); hipFree(b->cnt_cig); hipFree(b->off_hits); hipFree(b->off_cig); hipFree(b->unresolved);
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
     hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off); hipFree(b->d_intv);
+    hipFree(b->r_hits); hipFree(b->r_cig); hipFree(b->r_len); hipFree(b->r_text); hipFree(b->r_tmp); hipHostFree(b->r_host);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
     delete b;
@@ -1394,6 +1408,102 @@ extern "C" int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const
 }
 
 extern "C" const bsq_hits *bsq_batch_hits(const bsq_batch *b) { return b ? &b->view : nullptr; }
+
+// device buffer of at least `need` elements (contents not kept)
+template <typename T>
+static int grow_dev(T *&p, int64_t &cap, int64_t need)
+{
+    if (need <= cap) return BSQ_OK;
+    hipFree(p);
+    p = nullptr;
+    cap = std::max<int64_t>(need, cap + cap / 2);
+    HIPCHK(hipMalloc((void **)&p, (size_t)std::max<int64_t>(cap, 1) * sizeof(T)));
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len)
+{
+    if (!b || !text || !len) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *text = ""; *len = 0;
+    const bsq_hits &H = b->view;
+    if (H.n_hits <= 0) return BSQ_OK;
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t st = b->stream;
+    const HostIndex &h = b->idx->h;
+    { int rc = grow_dev(b->r_hits, b->r_hits_cap, H.n_hits); if (rc) return rc; }
+    { int rc = grow_dev(b->r_cig, b->r_cig_cap, std::max<int64_t>(H.n_cigar, 1)); if (rc) return rc; }
+    { int rc = grow_dev(b->r_len, b->r_len_cap, H.n_hits + 1); if (rc) return rc; }
+    HIPCHK(hipMemcpyAsync(b->r_hits, H.hits, (size_t)H.n_hits * sizeof(bsq_hit), hipMemcpyHostToDevice, st));
+    if (H.n_cigar) HIPCHK(hipMemcpyAsync(b->r_cig, H.cigar, (size_t)H.n_cigar * 4, hipMemcpyHostToDevice, st));
+    // reference holes by offset (the order field keeps the reference's overwrite order, Q3)
+    std::vector<RenderHole> rh;
+    int64_t hole_max = 0;
+    for (size_t i = 0; i < h.holes.size(); ++i) {
+        rh.push_back(RenderHole{h.holes[i].offset, h.holes[i].offset + h.holes[i].len, (uint32_t)i, (uint8_t)h.holes[i].amb});
+        hole_max = std::max<int64_t>(hole_max, h.holes[i].len);
+    }
+    std::sort(rh.begin(), rh.end(), [](const RenderHole &a, const RenderHole &c) { return a.beg < c.beg; });
+    // the reads' own hole symbols (nuclseq varlenas); without them, ambiguous bases print as N
+    std::vector<int64_t> qoff;
+    std::vector<RenderHole> qh;
+    if (reads) {
+        qoff.assign((size_t)H.n_reads + 1, 0);
+        for (int32_t r = 0; r < H.n_reads; ++r) {
+            const uint8_t *ns = static_cast<const uint8_t *>(reads[r]);
+            const uint32_t nh = ns ? ns_holes_num(ns) : 0;
+            for (uint32_t i = 0; i < nh; ++i) {
+                const Hole x = ns_hole(ns, i);
+                qh.push_back(RenderHole{x.offset, x.offset + x.len, i, (uint8_t)x.amb});
+            }
+            qoff[(size_t)r + 1] = (int64_t)qh.size();
+        }
+        if (qh.empty()) qoff.clear();
+    }
+    RenderHole *d_rh = nullptr, *d_qh = nullptr;
+    int64_t *d_qoff = nullptr;
+    struct Free { void *p[3]; ~Free() { for (void *q : p) if (q) hipFree(q); } } fr{{nullptr, nullptr, nullptr}};
+    if (!rh.empty()) {
+        HIPCHK(hipMalloc(&d_rh, rh.size() * sizeof(RenderHole))); fr.p[0] = d_rh;
+        HIPCHK(hipMemcpyAsync(d_rh, rh.data(), rh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
+    }
+    if (!qoff.empty()) {
+        HIPCHK(hipMalloc(&d_qh, qh.size() * sizeof(RenderHole))); fr.p[1] = d_qh;
+        HIPCHK(hipMalloc(&d_qoff, qoff.size() * 8)); fr.p[2] = d_qoff;
+        HIPCHK(hipMemcpyAsync(d_qh, qh.data(), qh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_qoff, qoff.data(), qoff.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    RenderView v{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int32_t)rh.size(), hole_max, b->codes,
+                 b->offs, d_qoff, d_qh};
+    HIPCHK(launch_row_len(st, v, b->r_len));
+    HIPCHK(hipMemsetAsync(b->r_len + H.n_hits, 0, 8, st));
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, b->r_len, b->r_len, (int)(H.n_hits + 1), st));
+    if (tb > b->r_tmp_bytes) {
+        hipFree(b->r_tmp);
+        b->r_tmp = nullptr;
+        HIPCHK(hipMalloc(&b->r_tmp, tb));
+        b->r_tmp_bytes = tb;
+    }
+    tb = b->r_tmp_bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(b->r_tmp, tb, b->r_len, b->r_len, (int)(H.n_hits + 1), st));
+    int64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, b->r_len + H.n_hits, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    { int rc = grow_dev(b->r_text, b->r_text_cap, total + 1); if (rc) return rc; }
+    if (total + 1 > b->r_host_cap) {
+        hipHostFree(b->r_host);
+        b->r_host = nullptr;
+        b->r_host_cap = std::max<int64_t>(total + 1, b->r_host_cap + b->r_host_cap / 2);
+        HIPCHK(hipHostMalloc((void **)&b->r_host, (size_t)b->r_host_cap));
+    }
+    HIPCHK(launch_row_write(st, v, b->r_len, b->r_text));
+    HIPCHK(hipMemcpyAsync(b->r_host, b->r_text, (size_t)total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    b->r_host[total] = 0;
+    *text = b->r_host;
+    *len = total;
+    return BSQ_OK;
+}
 
 extern "C" int bsq_batch_stage_ms(const bsq_batch *b, float *ms, int max)
 {

@@ -173,6 +173,11 @@ int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts);
  * it for SMEMs; nothing on the alignment path reads it).  Borrowed arrays, valid until the next call
  * on the batch. */
 int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const uint64_t **intv, int64_t *n_intv);
+/* The last run's rows rendered on the GPU as bwa_result text: the same bytes as bsq_render_tsv
+ * (SURVEY.md 8(f) row 2).  `reads` are the batch's reads as nuclseq varlenas, for the symbols of their
+ * holes (NULL: ambiguous bases print as N).  *text is borrowed (NUL-terminated, *len bytes), valid until
+ * the next run, render or free of the batch. */
+int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
 /* Per-stage device time of the last run in ms, measured with HIP events on the batch stream.

@@ -1,0 +1,66 @@
+"""bwa_result rows rendered on the GPU (bsq_batch_render) are byte-identical to
+the host renderer (bsq_render_tsv): reference rows with N/IUPAC runs (Q3 overlay), reverse-strand rows
+(Q7), clips printed as N (Q8), reads with IUPAC symbols, multi-chunk batches."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from bioseqdb_amd import NucleotideSequence, synth
+from bioseqdb_amd import _native as N
+from parity_util import build_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _reads_with_iupac(reads, r):
+    out = []
+    for i in range(reads.n):
+        t = list(reads.text(i))
+        if i % 7 == 0:
+            for _ in range(r.randrange(1, 3)):
+                p = r.randrange(0, len(t) - 4)
+                t[p:p + r.randrange(1, 4)] = r.choice("RYKNW")
+        out.append("".join(t))
+    return out
+
+
+@pytest.mark.parametrize("chunk", [None, "700"])
+def test_gpu_render_matches_host(monkeypatch, chunk):
+    if chunk:
+        monkeypatch.setenv("BSQ_CHUNK", chunk)
+    r = random.Random(17)
+    ref = synth.make_reference(400_000, n_rows=3, n_run_every=100_000, n_run_len=300)
+    texts = [t.decode() for t in ref.texts()]
+    texts[1] = texts[1][:5000] + "RRYY" + texts[1][5004:9000] + "N" * 40 + texts[1][9040:]
+    pi, _ = build_pair(texts)
+    pi.upload()
+    reads = synth.make_reads(ref, 2500, seed=29)
+    rtexts = _reads_with_iupac(reads, r)
+    seqs = [NucleotideSequence.from_text(t) for t in rtexts]
+    codes = np.concatenate([np.frombuffer(t.encode(), np.uint8) for t in rtexts])
+    lut = np.full(256, 4, np.uint8)
+    for c, v in zip(b"ACGT", range(4)):
+        lut[c] = v
+    codes = np.ascontiguousarray(lut[codes])
+    offs = np.zeros(len(rtexts) + 1, np.int64)
+    offs[1:] = np.cumsum([len(t) for t in rtexts])
+    L = N.lib()
+    b = ctypes.c_void_p()
+    N.check(L.bsq_batch_create(pi.handle, len(rtexts), int(offs[-1]), ctypes.byref(b)))
+    try:
+        N.check(L.bsq_batch_set_reads(b, codes.ctypes.data, offs.ctypes.data, len(rtexts)))
+        N.check(L.bsq_batch_run(b, ctypes.byref(pi.options), 0))
+        arr = (ctypes.c_void_p * len(seqs))(*[s.ptr for s in seqs])
+        p = L.bsq_render_tsv(pi.handle, L.bsq_batch_hits(b), arr)
+        host = ctypes.string_at(p)
+        L.bsq_free(p)
+        t, n = ctypes.c_void_p(), ctypes.c_int64()
+        N.check(L.bsq_batch_render(b, arr, ctypes.byref(t), ctypes.byref(n)))
+        gpu = ctypes.string_at(t, n.value)
+        assert n.value == len(host) and host.count(b"\n") >= 2000
+        assert gpu == host
+        assert b"\tf\tf\tt\t" in gpu or b"\tt\tf\tt\t" in gpu   # reverse-strand rows present
+    finally:
+        L.bsq_batch_free(b)
