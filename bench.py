@@ -103,14 +103,15 @@ def fnv_vec(h: np.ndarray, v: np.ndarray) -> np.ndarray:
     return h
 
 
-def gpu_checksum_vec(H, n_reads: int) -> int:
-    """The oracle's orc_align_batch checksum (per-read FNV, summed), vectorised over reads."""
+def gpu_checksum_vec(H, n_reads: int, read_base: int = 0) -> int:
+    """The oracle's orc_align_batch checksum (per-read FNV, summed), vectorised over reads; the batch's
+    read r is read read_base + r of the oracle's run."""
     off = np.ctypeslib.as_array(H.read_off, shape=(n_reads + 1,)).astype(np.int64)
     nh = int(off[n_reads] - off[0])
     hits = np.ctypeslib.as_array(H.hits, shape=(max(nh, 1),))[:nh] if nh else None
     ncig = int(H.n_cigar)
     cig = np.ctypeslib.as_array(H.cigar, shape=(max(ncig, 1),)) if ncig else np.zeros(1, np.uint32)
-    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64), np.arange(n_reads, dtype=np.uint64))
+    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64), np.arange(read_base, read_base + n_reads, dtype=np.uint64))
     cnt = off[1:] - off[:-1]
     for k in range(int(cnt.max()) if n_reads else 0):
         m = cnt > k
@@ -224,6 +225,8 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="concurrent batches per GPU (bsq_batch_run_many); each aligns 1/S of the reads")
     ap.add_argument("--index-build", default="device", choices=["device", "host"],
                     help="where the index is built before the timed region (device: bsq_index_build_device)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -293,13 +296,28 @@ def main() -> int:
     t_upload = time.time() - t0
     opts = default_opts(int(L.bsq_index_n_refs(idx)))
 
-    # ---- batch: reads resident in HBM before timing ----
-    batch = ctypes.c_void_p()
-    N.check(L.bsq_batch_create(idx, reads.n, int(reads.offsets[-1]), ctypes.byref(batch)))
-    codes = np.ascontiguousarray(reads.codes)
+    # ---- batches: reads resident in HBM before timing.  S batches over contiguous read ranges run
+    # concurrently (bsq_batch_run_many: one stream + host thread each); the stages of one fill the tails
+    # and host gaps of the others.  Every read is aligned exactly once per step. ----
+    S = 1 if cfg["seeding"] else max(1, args.streams)
+    lo_k = [reads.n * k // S for k in range(S + 1)]
+    subs = [reads.subset(lo_k[k], lo_k[k + 1]) for k in range(S)]
+    batches = []
+    keep_arrays = []
+    for sub in subs:
+        b = ctypes.c_void_p()
+        N.check(L.bsq_batch_create(idx, sub.n, int(sub.offsets[-1]), ctypes.byref(b)))
+        c_ = np.ascontiguousarray(sub.codes)
+        o_ = np.ascontiguousarray(sub.offsets)
+        keep_arrays += [c_, o_]
+        N.check(L.bsq_batch_set_reads(b, c_.ctypes.data, o_.ctypes.data, sub.n))
+        batches.append(b)
+    batch = batches[0]
+    codes = np.ascontiguousarray(reads.codes)     # the whole batch, for the CPU baseline
     offs = np.ascontiguousarray(reads.offsets)
-    N.check(L.bsq_batch_set_reads(batch, codes.ctypes.data, offs.ctypes.data, reads.n))
-    first_call = rank * reads.n    # lrand48 stream position as one backend aligning all ranks' reads in order
+    first_call = rank * reads.n   # lrand48 stream position as one backend aligning all ranks' reads in order
+    b_arr = (ctypes.c_void_p * S)(*[b.value for b in batches])
+    fc_arr = (ctypes.c_uint64 * S)(*[first_call + lo_k[k] for k in range(S)])
     log(f"[bench r{rank}] gen {t_gen:.1f}s index build {t_build:.1f}s upload {t_upload:.2f}s "
         f"seq_len {L.bsq_index_seq_len(idx)}")
 
@@ -307,16 +325,21 @@ def main() -> int:
         if cfg["seeding"]:
             N.check(L.bsq_batch_seed(batch, ctypes.byref(opts)))
             return
-        N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
+        if S == 1:
+            N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
+        else:
+            N.check(L.bsq_batch_run_many(b_arr, S, ctypes.byref(opts), fc_arr))
         if dist is not None:   # exchange step: hit records + CIGARs of every rank to the caller
             import torch
             from bioseqdb_amd import dist as D
-            H = L.bsq_batch_hits(batch).contents
-            nb = H.n_hits * ctypes.sizeof(N.Hit)
-            nc = H.n_cigar * 4
-            hb = np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb]
-            cb = np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc]
-            D.gather_records(np.concatenate([hb, cb]), device=xdev)
+            parts = []
+            for b in batches:   # batch order == read order
+                H = L.bsq_batch_hits(b).contents
+                nb = H.n_hits * ctypes.sizeof(N.Hit)
+                nc = H.n_cigar * 4
+                parts.append(np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb])
+                parts.append(np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc])
+            D.gather_records(np.concatenate(parts), device=xdev)
 
     hb.phase = "aligning"
     for _ in range(args.warmup):
@@ -331,15 +354,16 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        ms = (ctypes.c_float * 6)()
-        L.bsq_batch_stage_ms(batch, ms, 6)
-        by = (ctypes.c_double * 6)()
-        L.bsq_batch_stage_bytes(batch, by, 6)
-        wk = (ctypes.c_double * 6)()
-        L.bsq_batch_stage_work(batch, wk, 6)
-        stage_work += np.array(list(wk))
-        stage_ms += np.array(list(ms))
-        stage_bytes += np.array(list(by))
+        for b in batches:   # per-launch figures: averaged over the S concurrent launches of each stage
+            ms = (ctypes.c_float * 6)()
+            L.bsq_batch_stage_ms(b, ms, 6)
+            by = (ctypes.c_double * 6)()
+            L.bsq_batch_stage_bytes(b, by, 6)
+            wk = (ctypes.c_double * 6)()
+            L.bsq_batch_stage_work(b, wk, 6)
+            stage_work += np.array(list(wk))
+            stage_ms += np.array(list(ms))
+            stage_bytes += np.array(list(by))
     if dist is not None:
         import torch
         torch.cuda.synchronize()
@@ -350,16 +374,16 @@ def main() -> int:
         t = torch.tensor([elapsed], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stage_ms /= max(args.steps, 1)
-    stage_bytes /= max(args.steps, 1)
-    stage_work /= max(args.steps, 1)
-    H = L.bsq_batch_hits(batch).contents
-    n_hits = int(H.n_hits) if not cfg["seeding"] else 0
-    retried = int(L.bsq_batch_retried(batch))
+    stage_ms /= max(args.steps, 1) * S
+    stage_bytes /= max(args.steps, 1) * S
+    stage_work /= max(args.steps, 1) * S
+    reads_per_launch = reads.n / S
+    n_hits = sum(int(L.bsq_batch_hits(b).contents.n_hits) for b in batches) if not cfg["seeding"] else 0
+    retried = sum(int(L.bsq_batch_retried(b)) for b in batches)
     names = [L.bsq_stage_name(i).decode() for i in range(6)]
     kern = {names[i]: float(stage_ms[i]) for i in range(1 if cfg["seeding"] else 4)}
     # measured PMC traffic exists for the default C3 shape only (profiles/traffic.json)
-    tr = (lambda stage: traffic_for(stage, args.reads)) if (args.config == "c3" and default_shape) else \
+    tr = (lambda stage: traffic_for(stage, reads_per_launch)) if (args.config == "c3" and default_shape) else \
         (lambda stage: (None, None))
     dom = max(kern, key=kern.get)
     di = names.index(dom)
@@ -384,6 +408,7 @@ def main() -> int:
             "workload": cfg["label"],
             "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
             "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
+            "streams": S, "reads_per_launch": int(round(reads_per_launch)),
         },
         "roofline": {
             "bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -414,23 +439,40 @@ def main() -> int:
     if rank == 0 and not cfg["seeding"] and n_hits:
         hb.phase = "rendering rows on the host"
         keep, ptrs = reads_as_nuclseq(L, reads)
+        base = ctypes.addressof(ptrs)
+        sub_ptrs = [ctypes.cast(base + lo_k[k] * ctypes.sizeof(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
+                    for k in range(S)]   # sub-batch k's reads (its read_index is local)
+
+        def host_render():
+            n = 0
+            for k, b in enumerate(batches):
+                p = L.bsq_render_tsv(idx, L.bsq_batch_hits(b), sub_ptrs[k])
+                n += len(ctypes.string_at(p)) if p else 0
+                L.bsq_free(p)
+            return n
+
+        def gpu_render():
+            n = 0
+            tt, tn = ctypes.c_void_p(), ctypes.c_int64()
+            for k, b in enumerate(batches):
+                N.check(L.bsq_batch_render(b, sub_ptrs[k], ctypes.byref(tt), ctypes.byref(tn)))
+                n += int(tn.value)
+            return n
+
         t1 = time.perf_counter()
-        p = L.bsq_render_tsv(idx, L.bsq_batch_hits(batch), ptrs)
+        nbytes = host_render()
         dt_r = time.perf_counter() - t1
-        nbytes = len(ctypes.string_at(p)) if p else 0
-        L.bsq_free(p)
         os.environ["BSQ_RENDER_THREADS"] = "1"   # the reference's single-backend rendering, for comparison
         t1 = time.perf_counter()
-        L.bsq_free(L.bsq_render_tsv(idx, L.bsq_batch_hits(batch), ptrs))
+        host_render()
         dt_1 = time.perf_counter() - t1
         del os.environ["BSQ_RENDER_THREADS"]
-        tt, tn = ctypes.c_void_p(), ctypes.c_int64()
-        N.check(L.bsq_batch_render(batch, ptrs, ctypes.byref(tt), ctypes.byref(tn)))   # warm (buffers)
+        gpu_render()   # warm (buffers)
         t1 = time.perf_counter()
-        N.check(L.bsq_batch_render(batch, ptrs, ctypes.byref(tt), ctypes.byref(tn)))
+        gbytes = gpu_render()
         dt_g = time.perf_counter() - t1
         result["gpu_render"] = {"rows": n_hits, "seconds": round(dt_g, 4), "rows_per_s": round(n_hits / dt_g, 1),
-                                "text_MB": round(tn.value / 1e6, 1), "same_bytes_as_host": int(tn.value) == nbytes,
+                                "text_MB": round(gbytes / 1e6, 1), "same_bytes_as_host": gbytes == nbytes,
                                 "note": "bsq_batch_render: rows rendered on the GPU incl. record upload and text D2H"}
         result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
                                  "rows_per_s_1thread": round(n_hits / dt_1, 1),
@@ -482,7 +524,12 @@ def main() -> int:
             siv = np.ctypeslib.as_array(ivp, shape=(max(int(nt.value), 1) * 4,))[: int(nt.value) * 4].reshape(-1, 4)
             gck = intv_checksum_vec(soff, siv, sample)
         else:
-            gck = gpu_checksum_vec(H, sample)
+            gck = 0
+            for k, b in enumerate(batches):   # sub-batch k holds reads [lo_k[k], lo_k[k+1])
+                m = min(sample, lo_k[k + 1]) - lo_k[k]
+                if m > 0:
+                    gck += gpu_checksum_vec(L.bsq_batch_hits(b).contents, m, lo_k[k])
+            gck &= 0xFFFFFFFFFFFFFFFF
         result["cpu_baseline"] = {
             "value": round(sample / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} reads of the same batch, CPU oracle (oracle/bwa_oracle.c, -O2), "
@@ -501,7 +548,7 @@ def main() -> int:
         rf = result["roofline"]
         ki = names.index(dom)
         if ki < (1 if cfg["seeding"] else 4):
-            alg = per_read[ki] * args.reads
+            alg = per_read[ki] * reads_per_launch
             rf["issued_bytes_per_launch"] = rf.pop("algorithmic_bytes_per_launch")
             rf["issued_gbs"] = rf["achieved"]
             rf["frac_issued"] = rf["frac"]
@@ -514,12 +561,14 @@ def main() -> int:
             rf["frac"] = round(rf["achieved"] / HBM_PEAK_GBS, 5)
         for i, nm in enumerate(names[:1 if cfg["seeding"] else 4]):
             k = result["kernels"][STAGE_KERNEL[nm]]
-            k["algorithmic_bytes_8d"] = per_read[i] * args.reads
-            k["achieved_gbs_8d"] = round(per_read[i] * args.reads / (k["ms"] * 1e-3) / 1e9, 2) if k["ms"] > 0 else 0.0
+            k["algorithmic_bytes_8d"] = per_read[i] * reads_per_launch
+            k["achieved_gbs_8d"] = (round(per_read[i] * reads_per_launch / (k["ms"] * 1e-3) / 1e9, 2)
+                                    if k["ms"] > 0 else 0.0)
     hb.stop()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    L.bsq_batch_free(batch)
+    for b in batches:
+        L.bsq_batch_free(b)
     L.bsq_index_free(idx)
     if dist is not None:
         dist.destroy_process_group()

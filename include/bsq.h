@@ -178,6 +178,10 @@ int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const uint64_t *
  * holes (NULL: ambiguous bases print as N).  *text is borrowed (NUL-terminated, *len bytes), valid until
  * the next run, render or free of the batch. */
 int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len);
+/* Runs n batches concurrently (one host thread and HIP stream each); batch i draws lrand48 values from
+ * first_call[i].  Each batch keeps its own result view.  Returns the first error, prefixed by the batch
+ * index. */
+int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
 /* Per-stage device time of the last run in ms, measured with HIP events on the batch stream.

@@ -36,7 +36,11 @@ def main(root, dst, tag):
     calib = {names[i]: round(c[2] / (gib if i != 3 else 96 * (1 << 20)), 4) for i, c in enumerate(cal[:6])}
     corr = calib.get("gather64_4G", 1.0)
     fetch, write = per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE"), per_dispatch(os.path.join(root, "write"), "WRITE_SIZE")
-    res = {"round": tag, "reads_per_launch": 1000000, "fetch_correction": 1.0 / corr,
+    try:   # reads one launch of each stage processed in the profiled bench run (1M / --streams)
+        rpl = json.load(open(os.path.join(root, "fetch.json")))["config"]["reads_per_launch"]
+    except (OSError, KeyError, ValueError):
+        rpl = 1000000
+    res = {"round": tag, "reads_per_launch": rpl, "fetch_correction": 1.0 / corr,
            "calibration_fetch_size_over_bytes": calib, "kernels": {}}
     for stage, pats in KERNELS.items():
         fb = wb = 0.0
