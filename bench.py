@@ -416,6 +416,8 @@ def main() -> int:
             "traffic_source": (f"profiles/traffic.json ({tr(dom)[1]} PMC FETCH_SIZE+WRITE_SIZE per launch)"
                                if tr(dom)[0] else "not measured for this shape"),
             "algorithmic_bytes_per_launch": float(stage_bytes[di]), "launch_ms": round(float(stage_ms[di]), 3),
+            "launches": (f"{S} concurrent batches of {int(round(reads_per_launch))} reads; launch_ms is the kernel's "
+                         "duration while it shares the CUs with the other batches' stages" if S > 1 else "one batch"),
         },
         "kernels": {
             STAGE_KERNEL[nm]: {
