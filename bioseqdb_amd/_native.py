@@ -111,6 +111,13 @@ SIGNATURES = {
     "bsq_batch_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "bsq_index_download": (ctypes.c_int, [_P]),
     "bsq_index_build_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)]),
+    "bsq_nuclseq_encode_batch": (ctypes.c_int, [ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "bsq_nuclseq_decode_batch": (ctypes.c_int, [ctypes.c_int, _P, ctypes.c_int64, ctypes.POINTER(_P),
+                                                ctypes.POINTER(_P)]),
+    "bsq_nuclseq_codec_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "bsq_fasta_parse": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                       ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _lib = None

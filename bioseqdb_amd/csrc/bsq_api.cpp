@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -71,6 +72,15 @@ hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *);
 hipError_t launch_intv_counts(hipStream_t, int, const int32_t *, const uint32_t *, int64_t *);
 hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *, const uint32_t *, const int64_t *,
                             uint64_t *);
+// codec_gpu.hip
+struct EncView { const uint8_t *text; const int64_t *toff; const int64_t *poff; int64_t n, slots; int validate; };
+struct DecView { const uint8_t *in; const int64_t *in_off; const int64_t *poff; const int64_t *toff; int64_t n, slots; };
+hipError_t launch_enc_count(hipStream_t, const EncView &, int64_t, int64_t *, int64_t *, uint32_t *, unsigned long long *);
+hipError_t launch_enc_meta(hipStream_t, const EncView &, const int64_t *, const int64_t *, int64_t, const uint32_t *,
+                           int64_t *, int64_t *, int64_t *);
+hipError_t launch_enc_write(hipStream_t, const EncView &, int64_t, const int64_t *, const int64_t *, const int64_t *,
+                            const int64_t *, const int64_t *, int64_t, uint8_t *);
+hipError_t launch_dec(hipStream_t, const DecView &, const int64_t *, int64_t, char *);
 }  // namespace bsq
 
 using namespace bsq;
@@ -1595,4 +1605,228 @@ extern "C" void bsq_hits_free(bsq_hits *h)
 {
     if (!h) return;
     free(h->hits); free(h->cigar); free(h->read_off); free(h);
+}
+
+// ================================================================================================
+// bulk nuclseq codec on the GPU (codec_gpu.hip)
+// ================================================================================================
+namespace {
+struct DevAllocs {   // device buffers of one call, released on every return path
+    std::vector<void *> p;
+    ~DevAllocs() { for (void *q : p) hipFree(q); }
+    template <typename T>
+    hipError_t get(T *&out, size_t count)
+    {
+        void *q = nullptr;
+        const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(q);
+        out = static_cast<T *>(q);
+        return e;
+    }
+};
+struct OwnStream {
+    hipStream_t s = nullptr;
+    ~OwnStream() { if (s) hipStreamDestroy(s); }
+};
+thread_local double g_codec_ms[2];   // last call: kernels, whole call
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool allowed_host(unsigned char c) { return c && strchr("ACGTNWSMKRYBDHV", c) != nullptr; }
+
+int codec_device(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (device < 0 || device >= ndev) {
+        set_err("no HIP device %d (found %d); the bulk codec has no CPU fallback (bsq_nuclseq_from_text / _to_text "
+                "are the per-value host path)", device, ndev);
+        return BSQ_E_NODEV;
+    }
+    HIPCHK(hipSetDevice(device));
+    return BSQ_OK;
+}
+}  // namespace
+
+extern "C" int bsq_nuclseq_encode_batch(int device, const char *text, const int64_t *offs, int64_t n, int validate,
+                                        uint8_t **out, int64_t **out_off)
+{
+    if (!offs || n < 0 || n >= INT32_MAX || !out || !out_off) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *out = nullptr; *out_off = nullptr;
+    const double t_call = now_ms();
+    std::vector<int64_t> toff((size_t)n + 1, 0), poff((size_t)n + 1, 0);
+    int64_t first_long = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = offs[i + 1] - offs[i];
+        if (len < 0) { set_err("text offsets decrease at text %lld", (long long)i); return BSQ_E_INVALID; }
+        if (len > INT32_MAX / 4 && first_long < 0) first_long = i;
+        toff[(size_t)i + 1] = toff[(size_t)i] + len;
+        poff[(size_t)i + 1] = poff[(size_t)i] + (len + 3) / 4;
+    }
+    if (toff[(size_t)n] && !text) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (first_long >= 0) {   // nuclseq_in checks the length before the alphabet (extension.cpp:50-58)
+        for (int64_t i = 0; validate && i < first_long; ++i)
+            for (int64_t j = offs[i]; j < offs[i + 1]; ++j)
+                if (!allowed_host((unsigned char)text[j])) {
+                    set_err("invalid nucleotide in nuclseq_in: '%c'", text[j]);
+                    return BSQ_E_INVALID;
+                }
+        set_err("provided sequence is too long");
+        return BSQ_E_INVALID;
+    }
+    { const int rc = codec_device(device); if (rc) return rc; }
+    OwnStream os;
+    HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    hipStream_t st = os.s;
+    const int64_t T = toff[(size_t)n], slots = poff[(size_t)n], ntiles = (slots + 255) / 256;
+    if (ntiles + 1 >= INT32_MAX) { set_err("batch too large (%lld pac bytes)", (long long)slots); return BSQ_E_INVALID; }
+    DevAllocs da;
+    uint8_t *d_text, *d_out;
+    int64_t *d_toff, *d_poff, *tile_hb, *tile_hs, *hb_base, *hs_base, *d_off;
+    uint32_t *loc;
+    unsigned long long *bad;
+    HIPCHK(da.get(d_text, (size_t)T));
+    HIPCHK(da.get(d_toff, (size_t)n + 1));
+    HIPCHK(da.get(d_poff, (size_t)n + 1));
+    HIPCHK(da.get(tile_hb, (size_t)ntiles + 1));
+    HIPCHK(da.get(tile_hs, (size_t)ntiles + 1));
+    HIPCHK(da.get(hb_base, (size_t)n + 1));
+    HIPCHK(da.get(hs_base, (size_t)n + 1));
+    HIPCHK(da.get(d_off, (size_t)n + 1));
+    HIPCHK(da.get(loc, (size_t)n + 1));
+    HIPCHK(da.get(bad, 1));
+    if (T) HIPCHK(hipMemcpyAsync(d_text, text + offs[0], (size_t)T, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(tile_hb, 0, ((size_t)ntiles + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(tile_hs, 0, ((size_t)ntiles + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(bad, 0xff, 8, st));
+    hipEvent_t ev[4];
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 4; ++i) hipEventDestroy(e[i]); } } evf{ev};
+    const EncView v{d_text, d_toff, d_poff, n, slots, validate ? 1 : 0};
+    HIPCHK(hipEventRecord(ev[0], st));
+    HIPCHK(launch_enc_count(st, v, ntiles, tile_hb, tile_hs, loc, bad));
+    size_t tb = 0, tb2 = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, d_off, d_off, (int)(n + 1), st));
+    uint8_t *cub = nullptr;
+    HIPCHK(da.get(cub, std::max(tb, tb2)));
+    tb = std::max(tb, tb2);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hs, tile_hs, (int)(ntiles + 1), st));
+    HIPCHK(launch_enc_meta(st, v, tile_hb, tile_hs, ntiles, loc, hb_base, hs_base, d_off));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_off, d_off, (int)(n + 1), st));
+    int64_t tot[2] = {0, 0};
+    unsigned long long first_bad = ~0ull;
+    HIPCHK(hipEventRecord(ev[1], st));
+    HIPCHK(hipMemcpyAsync(&tot[0], d_off + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&tot[1], hs_base + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (validate && first_bad != ~0ull) {   // the first text (in order) with a character nuclseq_in rejects
+        set_err("invalid nucleotide in nuclseq_in: '%c'", text[offs[0] + (int64_t)first_bad]);
+        return BSQ_E_INVALID;
+    }
+    HIPCHK(da.get(d_out, (size_t)tot[0]));
+    HIPCHK(hipEventRecord(ev[2], st));
+    HIPCHK(launch_enc_write(st, v, ntiles, tile_hb, tile_hs, hb_base, hs_base, d_off, tot[1], d_out));
+    HIPCHK(hipEventRecord(ev[3], st));
+    uint8_t *h_out = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(tot[0], 1)));
+    int64_t *h_off = static_cast<int64_t *>(malloc(((size_t)n + 1) * 8));
+    if (!h_out || !h_off) { free(h_out); free(h_off); set_err("out of host memory"); return BSQ_E_NOMEM; }
+    hipError_t e = hipMemcpyAsync(h_out, d_out, (size_t)tot[0], hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_off, d_off, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { free(h_out); free(h_off); set_err("encode: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
+    float a = 0, b = 0;
+    hipEventElapsedTime(&a, ev[0], ev[1]);
+    hipEventElapsedTime(&b, ev[2], ev[3]);
+    g_codec_ms[0] = a + b;
+    g_codec_ms[1] = now_ms() - t_call;
+    *out = h_out;
+    *out_off = h_off;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_nuclseq_decode_batch(int device, const void *const *nuclseqs, int64_t n, char **text,
+                                        int64_t **text_off)
+{
+    if (n < 0 || (n > 0 && !nuclseqs) || !text || !text_off) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *text = nullptr; *text_off = nullptr;
+    const double t_call = now_ms();
+    std::vector<int64_t> in_off((size_t)n + 1, 0), poff((size_t)n + 1, 0), toff((size_t)n + 1, 0), holed;
+    for (int64_t s = 0; s < n; ++s) {
+        const uint8_t *ns = static_cast<const uint8_t *>(nuclseqs[s]);
+        if (!ns) { set_err("nuclseq %lld is NULL", (long long)s); return BSQ_E_INVALID; }
+        uint32_t vl; memcpy(&vl, ns, 4);
+        const uint64_t size = vl >> 2, nh = ns_holes_num(ns), len = ns_len(ns);
+        const uint64_t need = 12 + 16 * nh + pac_byte_size(len);
+        if (size < need) {
+            set_err("nuclseq %lld: varlena of %llu bytes, %llu needed", (long long)s, (unsigned long long)size,
+                    (unsigned long long)need);
+            return BSQ_E_INVALID;
+        }
+        if (nh) holed.push_back(s);
+        in_off[(size_t)s + 1] = in_off[(size_t)s] + (int64_t)((need + 7) & ~7ull);
+        poff[(size_t)s + 1] = poff[(size_t)s] + (int64_t)pac_byte_size(len);
+        toff[(size_t)s + 1] = toff[(size_t)s] + (int64_t)len;
+    }
+    { const int rc = codec_device(device); if (rc) return rc; }
+    OwnStream os;
+    HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    hipStream_t st = os.s;
+    std::vector<uint8_t> packed((size_t)in_off[(size_t)n]);
+    for (int64_t s = 0; s < n; ++s)
+        memcpy(packed.data() + in_off[(size_t)s], nuclseqs[s],
+               12 + 16 * (size_t)ns_holes_num(static_cast<const uint8_t *>(nuclseqs[s])) +
+                   (size_t)(poff[(size_t)s + 1] - poff[(size_t)s]));
+    DevAllocs da;
+    uint8_t *d_in;
+    int64_t *d_in_off, *d_poff, *d_toff, *d_holed;
+    char *d_text;
+    HIPCHK(da.get(d_in, packed.size()));
+    HIPCHK(da.get(d_in_off, (size_t)n + 1));
+    HIPCHK(da.get(d_poff, (size_t)n + 1));
+    HIPCHK(da.get(d_toff, (size_t)n + 1));
+    HIPCHK(da.get(d_holed, holed.size()));
+    HIPCHK(da.get(d_text, (size_t)toff[(size_t)n]));
+    if (!packed.empty()) HIPCHK(hipMemcpyAsync(d_in, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_in_off, in_off.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (!holed.empty()) HIPCHK(hipMemcpyAsync(d_holed, holed.data(), holed.size() * 8, hipMemcpyHostToDevice, st));
+    hipEvent_t ev[2];
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    struct EvFree { hipEvent_t *e; ~EvFree() { hipEventDestroy(e[0]); hipEventDestroy(e[1]); } } evf{ev};
+    const DecView v{d_in, d_in_off, d_poff, d_toff, n, poff[(size_t)n]};
+    HIPCHK(hipEventRecord(ev[0], st));
+    HIPCHK(launch_dec(st, v, d_holed, (int64_t)holed.size(), d_text));
+    HIPCHK(hipEventRecord(ev[1], st));
+    char *h_text = static_cast<char *>(malloc((size_t)toff[(size_t)n] + 1));
+    int64_t *h_off = static_cast<int64_t *>(malloc(((size_t)n + 1) * 8));
+    if (!h_text || !h_off) { free(h_text); free(h_off); set_err("out of host memory"); return BSQ_E_NOMEM; }
+    hipError_t e = toff[(size_t)n] ? hipMemcpyAsync(h_text, d_text, (size_t)toff[(size_t)n], hipMemcpyDeviceToHost, st)
+                                   : hipSuccess;
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { free(h_text); free(h_off); set_err("decode: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
+    h_text[toff[(size_t)n]] = 0;
+    memcpy(h_off, toff.data(), ((size_t)n + 1) * 8);
+    float a = 0;
+    hipEventElapsedTime(&a, ev[0], ev[1]);
+    g_codec_ms[0] = a;
+    g_codec_ms[1] = now_ms() - t_call;
+    *text = h_text;
+    *text_off = h_off;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_nuclseq_codec_ms(double *kernel_ms, double *call_ms)
+{
+    if (kernel_ms) *kernel_ms = g_codec_ms[0];
+    if (call_ms) *call_ms = g_codec_ms[1];
+    return BSQ_OK;
 }

@@ -89,6 +89,27 @@ void *bsq_nuclseq_from_text(const char *text, size_t len, size_t *out_size);
 /* Renders a NucleotideSequence varlena as text (malloc'd, NUL-terminated). */
 char *bsq_nuclseq_to_text(const void *nuclseq);
 
+/* ---- bulk codec and loader ---- */
+/* nuclseq_in for a whole batch on `device` (extension.cpp:46-61 + nuclseq_from_text, sequence.cpp:209-245):
+ * text i is text[offs[i] - offs[0] .. offs[i+1] - offs[0]).  On success *out holds the n varlenas, varlena i
+ * at (*out_off)[i] (8-byte aligned; (*out_off)[n] = total bytes), byte-identical to bsq_nuclseq_from_text.
+ * A text longer than INT32_MAX/4 fails with "provided sequence is too long"; with validate != 0 a character
+ * outside ACGTNWSMKRYBDHV fails with "invalid nucleotide in nuclseq_in: '<c>'" -- the first failure in
+ * text order, as a cursor of nuclseq_in calls would raise it (BSQ_E_INVALID).  Both outputs are malloc'd
+ * (bsq_free).  No device: BSQ_E_NODEV (no CPU fallback). */
+int bsq_nuclseq_encode_batch(int device, const char *text, const int64_t *offs, int64_t n, int validate,
+                             uint8_t **out, int64_t **out_off);
+/* nuclseq_out for a whole batch (to_text_palloc, sequence.cpp:71-81,162-166): text i at
+ * (*text)[(*text_off)[i] .. (*text_off)[i+1]), *text NUL-terminated; both malloc'd (bsq_free). */
+int bsq_nuclseq_decode_batch(int device, const void *const *nuclseqs, int64_t n, char **text, int64_t **text_off);
+/* Device time of the last encode/decode call on this thread (kernels only) and the whole call's wall time. */
+int bsq_nuclseq_codec_ms(double *kernel_ms, double *call_ms);
+/* The FASTA reading of bioseqdb-import (bioseqdb-import/main.cpp:48-71): records split at '>' lines, sequence
+ * lines upper-cased and concatenated, empty records dropped.  Record i: sequence (*seq)[(*seq_off)[i] ..
+ * (*seq_off)[i+1]), name (*names)[(*name_off)[i] .. (*name_off)[i+1]).  All four outputs malloc'd. */
+int bsq_fasta_parse(const char *data, int64_t size, char **seq, int64_t **seq_off, char **names, int64_t **name_off,
+                    int64_t *n_records);
+
 /* ---- index ----------------------------------------------------------------------------------- */
 int bsq_index_create(bsq_index **out);
 void bsq_index_free(bsq_index *idx);
