@@ -111,7 +111,8 @@ def gpu_checksum_vec(H, n_reads: int, read_base: int = 0) -> int:
     hits = np.ctypeslib.as_array(H.hits, shape=(max(nh, 1),))[:nh] if nh else None
     ncig = int(H.n_cigar)
     cig = np.ctypeslib.as_array(H.cigar, shape=(max(ncig, 1),)) if ncig else np.zeros(1, np.uint32)
-    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64), np.arange(read_base, read_base + n_reads, dtype=np.uint64))
+    h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64),
+                np.arange(read_base, read_base + n_reads, dtype=np.uint64))
     cnt = off[1:] - off[:-1]
     for k in range(int(cnt.max()) if n_reads else 0):
         m = cnt > k
@@ -225,6 +226,7 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-codec", action="store_true", help="skip the bulk nuclseq codec measurement")
     ap.add_argument("--streams", type=int, default=3,
                     help="concurrent batches per GPU (bsq_batch_run_many); each aligns 1/S of the reads")
     ap.add_argument("--index-build", default="device", choices=["device", "host"],
@@ -482,6 +484,44 @@ def main() -> int:
                                  "note": "bsq_render_tsv of the last step (BwaMatch text, Q3/Q7/Q8 rules); "
                                          "outside the timed region"}
         del keep, ptrs
+
+    # ---- bulk codec: the reference rows through nuclseq_in on the GPU vs the
+    # per-value host codec, outside the timed region ----
+    if rank == 0 and not args.no_codec:
+        hb.phase = "bulk codec"
+        from bioseqdb_amd import loader
+        texts = ref.texts()
+        toffs = np.zeros(len(texts) + 1, dtype=np.int64)
+        toffs[1:] = np.cumsum([len(t) for t in texts])
+        tcat = np.frombuffer(b"".join(texts), dtype=np.uint8)
+        loader.encode_concat(tcat, toffs)   # warm
+        t1 = time.perf_counter()
+        raw, voff = loader.encode_concat(tcat, toffs)
+        dt_e = time.perf_counter() - t1
+        k_e, _ = loader.codec_ms()
+        vals = loader._split(raw, voff)
+        dt_h = 0.0
+        for t in texts:   # the per-value path (bsq_nuclseq_from_text = nuclseq_from_text), one host thread
+            size = ctypes.c_size_t()
+            t2 = time.perf_counter()
+            p = L.bsq_nuclseq_from_text(t, len(t), ctypes.byref(size))
+            dt_h += time.perf_counter() - t2
+            L.bsq_free(p)
+        same = all(v.raw == bytes(h.raw) for v, h in zip(vals, ref_ns)) if ref_ns else None
+        loader.nuclseq_out_batch(vals)
+        k_d, c_d = loader.codec_ms()
+        nb = int(toffs[-1])
+        out_b = int(voff[-1])
+        result["bulk_codec"] = {
+            "bases": nb, "encode_s": round(dt_e, 4), "encode_kernel_ms": round(k_e, 3),
+            "encode_kernel_gbs": round((2 * nb + out_b) / (k_e * 1e-3) / 1e9, 1) if k_e > 0 else None,
+            "encode_gbases_per_s": round(nb / dt_e / 1e9, 2), "host_gbases_per_s_1thread": round(nb / dt_h / 1e9, 3),
+            "decode_kernel_ms": round(k_d, 3), "decode_call_s": round(c_d * 1e-3, 4),
+            "same_bytes_as_host": same,
+            "note": "bsq_nuclseq_encode_batch on the reference rows (call incl. PCIe both ways); kernel GB/s counts "
+                    "the text read twice (count + write passes) and the varlenas written once",
+        }
+        del raw, vals, tcat
 
     # ---- CPU baseline: the oracle on this host, bounded sample, rank 0 at N = 1 only ----
     hb.phase = "CPU baseline"
