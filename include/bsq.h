@@ -39,7 +39,7 @@ extern "C" {
 #define BSQ_E_NOMEM (-2)     /* host or device allocation failed */
 #define BSQ_E_HIP (-3)       /* HIP runtime error */
 #define BSQ_E_NODEV (-4)     /* no usable gfx950 device */
-#define BSQ_E_UNSUPPORTED (-5) /* input outside what the path implements (e.g. reads >= 700 bp) */
+#define BSQ_E_UNSUPPORTED (-5) /* input outside what the path implements (a read beyond even the retry capacities) */
 
 /* Effective BWA-MEM options (mem_opt_t fields bioseqdb writes, extension.cpp:220-231).  The SQL
  * bwa_opts() field-order quirk (Q1) is applied by the caller: defaults are
