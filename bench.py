@@ -483,6 +483,19 @@ def main() -> int:
                                  "text_MB": round(nbytes / 1e6, 1), "threads": min(16, os.cpu_count() or 1),
                                  "note": "bsq_render_tsv of the last step (BwaMatch text, Q3/Q7/Q8 rules); "
                                          "outside the timed region"}
+        # the SQL-level call: one bsq_align_batch over the cursor's nuclseq values in
+        # host memory -- batch and workspace set-up, device nt4 conversion, alignment, record copy
+        hb.phase = "one-shot bsq_align_batch"
+        ho = ctypes.POINTER(N.Hits)()
+        t1 = time.perf_counter()
+        N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
+        dt_s = time.perf_counter() - t1
+        result["sql_batch_call"] = {
+            "reads": reads.n, "seconds": round(dt_s, 3), "reads_per_s": round(reads.n / dt_s, 1),
+            "same_rows": int(ho.contents.n_hits) == n_hits,
+            "note": "bsq_align_batch from nuclseq varlenas in host memory, one call (allocation, upload, device "
+                    "nt4 conversion, alignment, D2H of the records); the timed metric excludes set-up"}
+        L.bsq_hits_free(ho)
         del keep, ptrs
 
     # ---- bulk codec: the reference rows through nuclseq_in on the GPU vs the

@@ -81,6 +81,7 @@ hipError_t launch_enc_meta(hipStream_t, const EncView &, const int64_t *, const 
 hipError_t launch_enc_write(hipStream_t, const EncView &, int64_t, const int64_t *, const int64_t *, const int64_t *,
                             const int64_t *, const int64_t *, int64_t, uint8_t *);
 hipError_t launch_dec(hipStream_t, const DecView &, const int64_t *, int64_t, char *);
+hipError_t launch_dec_codes(hipStream_t, const DecView &, const int64_t *, int64_t, uint8_t *);
 }  // namespace bsq
 
 using namespace bsq;
@@ -748,7 +749,13 @@ struct bsq_batch {
     int64_t *offs = nullptr;
     int64_t *ids = nullptr;
     std::vector<int64_t> h_offs;
-    std::vector<uint8_t> h_codes;   // kept for the retry pass
+    std::vector<uint8_t> h_codes;   // staging copy of set_reads' codes
+    // bsq_batch_set_nuclseqs: packed varlenas and their offsets on the device (grown on demand)
+    std::vector<uint8_t> ns_host;
+    uint8_t *ns_dev = nullptr;
+    int64_t ns_dev_cap = 0;
+    int64_t *ns_meta = nullptr;   // in_off | poff | holed texts
+    int64_t ns_meta_cap = 0;
     Workspace main, retry;
     Counters *ctr = nullptr;
     // packing
@@ -883,10 +890,13 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
     hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off); hipFree(b->d_intv);
     hipFree(b->r_hits); hipFree(b->r_cig); hipFree(b->r_len); hipFree(b->r_text); hipFree(b->r_tmp); hipHostFree(b->r_host);
+    hipFree(b->ns_dev); hipFree(b->ns_meta);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
     delete b;
 }
+
+static int prepare_workspace(bsq_batch *b, int max_len);
 
 extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int64_t *offsets, int32_t n_reads)
 {
@@ -911,8 +921,15 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
         HIPCHK(hipMemcpyAsync(b->codes, b->h_codes.data(), (size_t)total, hipMemcpyHostToDevice, b->stream));
         HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (size_t)(n_reads + 1) * 8, hipMemcpyHostToDevice, b->stream));
     }
-    // (re)allocate the main workspace for this read length; the per-read slots grow with the length, so
-    // long reads run in proportionally smaller workspace passes (~ the bytes of 1M x 150 bp)
+    { const int rc = prepare_workspace(b, max_len); if (rc) return rc; }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return BSQ_OK;
+}
+
+// (re)allocate the main workspace for this read length; the per-read slots grow with the length, so
+// long reads run in proportionally smaller workspace passes (~ the bytes of 1M x 150 bp)
+static int prepare_workspace(bsq_batch *b, int max_len)
+{
     const int32_t want = max_len > 150 ? std::max<int32_t>(1, std::min<int64_t>(b->chunk0, (int64_t)b->chunk0 * 150 / max_len))
                                        : b->chunk0;
     if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1) || want != b->chunk) {
@@ -921,6 +938,58 @@ extern "C" int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int
         int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device), 32 * 1024, false);
         if (rc) return rc;
     }
+    return BSQ_OK;
+}
+
+template <typename T>
+static int grow_dev(T *&p, int64_t &cap, int64_t need);
+
+// Reads given as nuclseq varlenas (the cursor's detoasted values): the varlenas are
+// packed and uploaded as they are and turned into nt4 codes on the device (codec_gpu.hip, the same
+// pass as nuclseq_out with hole bases as code 4), instead of a per-read host conversion.
+extern "C" int bsq_batch_set_nuclseqs(bsq_batch *b, const void *const *reads, int32_t n_reads)
+{
+    if (!b || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (n_reads > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    const size_t n = (size_t)n_reads;
+    std::vector<int64_t> meta(2 * (n + 1), 0);   // in_off | poff, then the holed reads
+    int64_t *in_off = meta.data(), *poff = meta.data() + n + 1;
+    b->h_offs.assign(n + 1, 0);
+    int max_len = 0;
+    for (size_t s = 0; s < n; ++s) {
+        const uint8_t *ns = static_cast<const uint8_t *>(reads[s]);
+        if (!ns) { set_err("read %zu is NULL", s); return BSQ_E_INVALID; }
+        uint32_t vl; memcpy(&vl, ns, 4);
+        const uint64_t nh = ns_holes_num(ns), len = ns_len(ns), need = 12 + 16 * nh + pac_byte_size(len);
+        if ((vl >> 2) < need) { set_err("read %zu: varlena of %u bytes, %llu needed", s, vl >> 2, (unsigned long long)need); return BSQ_E_INVALID; }
+        if (nh) meta.push_back((int64_t)s);
+        in_off = meta.data(); poff = meta.data() + n + 1;
+        in_off[s + 1] = in_off[s] + (int64_t)((need + 7) & ~7ull);
+        poff[s + 1] = poff[s] + (int64_t)pac_byte_size(len);
+        b->h_offs[s + 1] = b->h_offs[s] + (int64_t)len;
+        max_len = std::max<int>(max_len, (int)len);
+    }
+    const int64_t total = b->h_offs[n];
+    if (total > b->max_bases) { set_err("batch holds at most %lld bases", (long long)b->max_bases); return BSQ_E_INVALID; }
+    b->ns_host.resize((size_t)in_off[n]);
+    for (size_t s = 0; s < n; ++s) {
+        const uint8_t *ns = static_cast<const uint8_t *>(reads[s]);
+        memcpy(b->ns_host.data() + in_off[s], ns, 12 + 16 * (size_t)ns_holes_num(ns) + (size_t)(poff[s + 1] - poff[s]));
+    }
+    { const int rc = grow_dev(b->ns_dev, b->ns_dev_cap, (int64_t)b->ns_host.size()); if (rc) return rc; }
+    { const int rc = grow_dev(b->ns_meta, b->ns_meta_cap, (int64_t)meta.size()); if (rc) return rc; }
+    b->n_reads = n_reads;
+    b->max_len = max_len;
+    if (n_reads) {
+        hipStream_t st = b->stream;
+        HIPCHK(hipMemcpyAsync(b->ns_dev, b->ns_host.data(), b->ns_host.size(), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->ns_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const DecView v{b->ns_dev, b->ns_meta, b->ns_meta + n + 1, b->offs, (int64_t)n, poff[n]};
+        HIPCHK(launch_dec_codes(st, v, b->ns_meta + 2 * (n + 1), (int64_t)(meta.size() - 2 * (n + 1)), b->codes));
+    }
+    { const int rc = prepare_workspace(b, max_len); if (rc) return rc; }
     HIPCHK(hipStreamSynchronize(b->stream));
     return BSQ_OK;
 }
@@ -1567,11 +1636,10 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
 {
     if (!idx || !opts || !out || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
     *out = nullptr;
-    std::vector<uint8_t> codes;
-    std::vector<int64_t> offs((size_t)n_reads + 1, 0);
+    int64_t n_bases = 0;
     for (int i = 0; i < n_reads; ++i) {
-        ns_to_nt4(static_cast<const uint8_t *>(reads[i]), codes);
-        offs[i + 1] = (int64_t)codes.size();
+        if (!reads[i]) { set_err("read %d is NULL", i); return BSQ_E_INVALID; }
+        n_bases += ns_len(static_cast<const uint8_t *>(reads[i]));
     }
     bsq_hits *h = (bsq_hits *)calloc(1, sizeof(bsq_hits));
     if (!h) { set_err("out of memory"); return BSQ_E_NOMEM; }
@@ -1584,8 +1652,8 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     }
     if (!idx->h.dev) { free(h); set_err("index not uploaded to a device (call bsq_index_upload)"); return BSQ_E_NODEV; }
     bsq_batch *b = nullptr;
-    int rc = bsq_batch_create(idx, n_reads, (int64_t)codes.size(), &b);
-    if (rc == BSQ_OK) rc = bsq_batch_set_reads(b, codes.data(), offs.data(), n_reads);
+    int rc = bsq_batch_create(idx, n_reads, n_bases, &b);
+    if (rc == BSQ_OK) rc = bsq_batch_set_nuclseqs(b, reads, n_reads);
     if (rc == BSQ_OK) rc = bsq_batch_run(b, opts, first_call_seq);
     if (rc != BSQ_OK) { bsq_batch_free(b); free(h); return rc; }
     h->n_hits = b->view.n_hits;

@@ -299,6 +299,8 @@ struct DecView {
     int64_t n, slots;
 };
 
+// CODES: nt4 codes (0..3, holes 4) for the alignment path instead of text
+template <bool CODES>
 __global__ void k_dec_bases(DecView v, char *out)
 {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < v.slots; g += (int64_t)gridDim.x * blockDim.x) {
@@ -308,11 +310,16 @@ __global__ void k_dec_bases(DecView v, char *out)
         const int64_t len = v.toff[s + 1] - v.toff[s], j = g - v.poff[s];
         const uint32_t byte = ns[12 + 16 * (int64_t)nh + j];
         char *o = out + v.toff[s] + 4 * j;
-        for (int k = 0; k < 4 && 4 * j + k < len; ++k) o[k] = "ACGT"[(byte >> ((3 - k) << 1)) & 3];
+        for (int k = 0; k < 4 && 4 * j + k < len; ++k) {
+            const uint32_t c = (byte >> ((3 - k) << 1)) & 3;
+            o[k] = CODES ? (char)c : "ACGT"[c];
+        }
     }
 }
 
-// one block per text with holes: holes in order, later ones overwrite (inplace_to_text :77-78)
+// one block per text with holes: holes in order, later ones overwrite (inplace_to_text :77-78); as nt4
+// codes every hole base is 4 (ns_to_nt4: hole symbols are never ACGT)
+template <bool CODES>
 __global__ void k_dec_holes(DecView v, const int64_t *texts, char *out)
 {
     const int64_t s = texts[blockIdx.x];
@@ -324,20 +331,32 @@ __global__ void k_dec_holes(DecView v, const int64_t *texts, char *out)
         const uint8_t *r = ns + 12 + 16 * (int64_t)h;
         const int64_t off = (int64_t)((uint64_t)ld32(r) | (uint64_t)ld32(r + 4) << 32);
         const int32_t hl = (int32_t)ld32(r + 8);
-        const char amb = (char)r[12];
+        const char amb = CODES ? (char)4 : (char)r[12];
         const int64_t a = off < 0 ? 0 : off, e = off + hl < len ? off + hl : len;
         for (int64_t i = a + threadIdx.x; i < e; i += blockDim.x) o[i] = amb;
         __syncthreads();
     }
 }
 
+template <bool CODES>
+static hipError_t dec(hipStream_t st, const DecView &v, const int64_t *hole_texts, int64_t n_hole_texts, char *out)
+{
+    if (v.slots) hipLaunchKernelGGL(k_dec_bases<CODES>, cgrid(v.slots), dim3(256), 0, st, v, out);
+    for (int64_t k = 0; k < n_hole_texts; k += 65535)   // one block per text with holes
+        hipLaunchKernelGGL(k_dec_holes<CODES>, dim3((unsigned)(n_hole_texts - k < 65535 ? n_hole_texts - k : 65535)),
+                           dim3(256), 0, st, v, hole_texts + k, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_dec(hipStream_t st, const DecView &v, const int64_t *hole_texts, int64_t n_hole_texts, char *out)
 {
-    if (v.slots) hipLaunchKernelGGL(k_dec_bases, cgrid(v.slots), dim3(256), 0, st, v, out);
-    for (int64_t k = 0; k < n_hole_texts; k += 65535)   // one block per text with holes
-        hipLaunchKernelGGL(k_dec_holes, dim3((unsigned)(n_hole_texts - k < 65535 ? n_hole_texts - k : 65535)), dim3(256),
-                           0, st, v, hole_texts + k, out);
-    return hipGetLastError();
+    return dec<false>(st, v, hole_texts, n_hole_texts, out);
+}
+
+hipError_t launch_dec_codes(hipStream_t st, const DecView &v, const int64_t *hole_texts, int64_t n_hole_texts,
+                            uint8_t *codes)
+{
+    return dec<true>(st, v, hole_texts, n_hole_texts, reinterpret_cast<char *>(codes));
 }
 
 }  // namespace bsq

@@ -182,6 +182,9 @@ int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_bases, bsq_b
 void bsq_batch_free(bsq_batch *b);
 /* Stage reads given as nt4 codes (0..3 = ACGT, 4 = other), offsets[n+1] (host arrays) into HBM. */
 int bsq_batch_set_reads(bsq_batch *b, const uint8_t *codes, const int64_t *offsets, int32_t n_reads);
+/* Stage reads given as nuclseq varlenas (the cursor's detoasted values): uploaded as they are and turned
+ * into nt4 codes on the device.  bsq_align_batch uses this path. */
+int bsq_batch_set_nuclseqs(bsq_batch *b, const void *const *reads, int32_t n_reads);
 /* Run the whole alignment pipeline on the staged reads and copy the packed hits to the host. */
 int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq);
 /* Seeding only (BASELINE.json configs[1]; libbwa mem_collect_intv as called by mem_align1_core,
