@@ -478,6 +478,18 @@ def main() -> int:
         result["gpu_render"] = {"rows": n_hits, "seconds": round(dt_g, 4), "rows_per_s": round(n_hits / dt_g, 1),
                                 "text_MB": round(gbytes / 1e6, 1), "same_bytes_as_host": gbytes == nbytes,
                                 "note": "bsq_batch_render: rows rendered on the GPU incl. record upload and text D2H"}
+
+        def gpu_columns():   # build_tuple_bwa's two nuclseq columns per row (bsq_batch_render_nuclseqs)
+            out, oo = ctypes.c_void_p(), ctypes.c_void_p()
+            for k, b in enumerate(batches):
+                N.check(L.bsq_batch_render_nuclseqs(b, sub_ptrs[k], ctypes.byref(out), ctypes.byref(oo)))
+                L.bsq_free(out)
+                L.bsq_free(oo)
+
+        gpu_columns()   # warm
+        t1 = time.perf_counter()
+        gpu_columns()
+        result["gpu_render"]["nuclseq_columns_rows_per_s"] = round(n_hits / (time.perf_counter() - t1), 1)
         result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
                                  "rows_per_s_1thread": round(n_hits / dt_1, 1),
                                  "text_MB": round(nbytes / 1e6, 1), "threads": min(16, os.cpu_count() or 1),

@@ -117,6 +117,7 @@ SIGNATURES = {
                                                 ctypes.POINTER(_P)]),
     "bsq_nuclseq_codec_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "bsq_batch_set_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
+    "bsq_batch_render_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "bsq_fasta_parse": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
 }

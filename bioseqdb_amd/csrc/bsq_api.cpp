@@ -66,6 +66,7 @@ struct RenderView {
 };
 hipError_t launch_row_len(hipStream_t, const RenderView &, int64_t *);
 hipError_t launch_row_write(hipStream_t, const RenderView &, const int64_t *, char *);
+hipError_t launch_sub_write(hipStream_t, const RenderView &, const int64_t *, char *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
 hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *);
@@ -1521,13 +1522,17 @@ static int grow_dev(T *&p, int64_t &cap, int64_t need)
     return BSQ_OK;
 }
 
-extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len)
+// device inputs of the GPU renderers: the last run's records, the reference holes by offset and the reads'
+// own holes (freed with the object)
+struct RenderInputs {
+    RenderView v{};
+    void *p[3] = {nullptr, nullptr, nullptr};
+    ~RenderInputs() { for (void *q : p) if (q) hipFree(q); }
+};
+
+static int render_inputs(bsq_batch *b, const void *const *reads, RenderInputs &ri)
 {
-    if (!b || !text || !len) { set_err("invalid argument"); return BSQ_E_INVALID; }
-    *text = ""; *len = 0;
     const bsq_hits &H = b->view;
-    if (H.n_hits <= 0) return BSQ_OK;
-    HIPCHK(hipSetDevice(b->device));
     hipStream_t st = b->stream;
     const HostIndex &h = b->idx->h;
     { int rc = grow_dev(b->r_hits, b->r_hits_cap, H.n_hits); if (rc) return rc; }
@@ -1561,19 +1566,33 @@ extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const ch
     }
     RenderHole *d_rh = nullptr, *d_qh = nullptr;
     int64_t *d_qoff = nullptr;
-    struct Free { void *p[3]; ~Free() { for (void *q : p) if (q) hipFree(q); } } fr{{nullptr, nullptr, nullptr}};
+    void **fr = ri.p;
     if (!rh.empty()) {
-        HIPCHK(hipMalloc(&d_rh, rh.size() * sizeof(RenderHole))); fr.p[0] = d_rh;
+        HIPCHK(hipMalloc(&d_rh, rh.size() * sizeof(RenderHole))); fr[0] = d_rh;
         HIPCHK(hipMemcpyAsync(d_rh, rh.data(), rh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
     }
     if (!qoff.empty()) {
-        HIPCHK(hipMalloc(&d_qh, qh.size() * sizeof(RenderHole))); fr.p[1] = d_qh;
-        HIPCHK(hipMalloc(&d_qoff, qoff.size() * 8)); fr.p[2] = d_qoff;
+        HIPCHK(hipMalloc(&d_qh, qh.size() * sizeof(RenderHole))); fr[1] = d_qh;
+        HIPCHK(hipMalloc(&d_qoff, qoff.size() * 8)); fr[2] = d_qoff;
         HIPCHK(hipMemcpyAsync(d_qh, qh.data(), qh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(d_qoff, qoff.data(), qoff.size() * 8, hipMemcpyHostToDevice, st));
     }
-    RenderView v{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int32_t)rh.size(), hole_max, b->codes,
-                 b->offs, d_qoff, d_qh};
+    ri.v = RenderView{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int32_t)rh.size(), hole_max, b->codes,
+                      b->offs, d_qoff, d_qh};
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len)
+{
+    if (!b || !text || !len) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *text = ""; *len = 0;
+    const bsq_hits &H = b->view;
+    if (H.n_hits <= 0) return BSQ_OK;
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t st = b->stream;
+    RenderInputs ri;
+    { const int rc = render_inputs(b, reads, ri); if (rc) return rc; }
+    const RenderView &v = ri.v;
     HIPCHK(launch_row_len(st, v, b->r_len));
     HIPCHK(hipMemsetAsync(b->r_len + H.n_hits, 0, 8, st));
     size_t tb = 0;
@@ -1719,6 +1738,86 @@ int codec_device(int device)
 }
 }  // namespace
 
+// nuclseq_from_text of n texts already in HBM (text i at d_text + toff[i], pac bytes poff[]): the varlenas
+// are written to *d_out at the device offsets *d_off (n+1, 8-byte aligned), *total bytes.  With validate,
+// a character nuclseq_in rejects stops before the write pass: *first_bad = its text offset (else ~0).
+static int encode_device(hipStream_t st, DevAllocs &da, const uint8_t *d_text, const std::vector<int64_t> &toff,
+                         const std::vector<int64_t> &poff, int64_t n, bool validate, uint8_t **d_out, int64_t **d_off,
+                         int64_t *total, unsigned long long *first_bad, double *kernel_ms)
+{
+    const int64_t slots = poff[(size_t)n], ntiles = (slots + 255) / 256;
+    if (ntiles + 1 >= INT32_MAX || n + 1 >= INT32_MAX) { set_err("batch too large (%lld pac bytes)", (long long)slots); return BSQ_E_INVALID; }
+    int64_t *d_toff, *d_poff, *tile_hb, *tile_hs, *hb_base, *hs_base, *off;
+    uint32_t *loc;
+    unsigned long long *bad;
+    HIPCHK(da.get(d_toff, (size_t)n + 1));
+    HIPCHK(da.get(d_poff, (size_t)n + 1));
+    HIPCHK(da.get(tile_hb, (size_t)ntiles + 1));
+    HIPCHK(da.get(tile_hs, (size_t)ntiles + 1));
+    HIPCHK(da.get(hb_base, (size_t)n + 1));
+    HIPCHK(da.get(hs_base, (size_t)n + 1));
+    HIPCHK(da.get(off, (size_t)n + 1));
+    HIPCHK(da.get(loc, (size_t)n + 1));
+    HIPCHK(da.get(bad, 1));
+    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(tile_hb, 0, ((size_t)ntiles + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(tile_hs, 0, ((size_t)ntiles + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(bad, 0xff, 8, st));
+    hipEvent_t ev[4];
+    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+    struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 4; ++i) hipEventDestroy(e[i]); } } evf{ev};
+    const EncView v{d_text, d_toff, d_poff, n, slots, validate ? 1 : 0};
+    HIPCHK(hipEventRecord(ev[0], st));
+    HIPCHK(launch_enc_count(st, v, ntiles, tile_hb, tile_hs, loc, bad));
+    size_t tb = 0, tb2 = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, off, off, (int)(n + 1), st));
+    uint8_t *cub = nullptr;
+    HIPCHK(da.get(cub, std::max(tb, tb2)));
+    tb = std::max(tb, tb2);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hs, tile_hs, (int)(ntiles + 1), st));
+    HIPCHK(launch_enc_meta(st, v, tile_hb, tile_hs, ntiles, loc, hb_base, hs_base, off));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, off, off, (int)(n + 1), st));
+    int64_t tot[2] = {0, 0};
+    HIPCHK(hipEventRecord(ev[1], st));
+    HIPCHK(hipMemcpyAsync(&tot[0], off + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&tot[1], hs_base + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(first_bad, bad, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *d_out = nullptr; *d_off = off; *total = tot[0];
+    if (validate && *first_bad != ~0ull) return BSQ_OK;
+    uint8_t *out;
+    HIPCHK(da.get(out, (size_t)tot[0]));
+    HIPCHK(hipEventRecord(ev[2], st));
+    HIPCHK(launch_enc_write(st, v, ntiles, tile_hb, tile_hs, hb_base, hs_base, off, tot[1], out));
+    HIPCHK(hipEventRecord(ev[3], st));
+    HIPCHK(hipStreamSynchronize(st));
+    float a = 0, c = 0;
+    hipEventElapsedTime(&a, ev[0], ev[1]);
+    hipEventElapsedTime(&c, ev[2], ev[3]);
+    *kernel_ms = a + c;
+    *d_out = out;
+    return BSQ_OK;
+}
+
+// copies n+1 offsets and the bytes they span from the device into malloc'd host arrays
+static int download(hipStream_t st, const uint8_t *d_buf, const int64_t *d_off, int64_t n, int64_t total, uint8_t **buf,
+                    int64_t **offs)
+{
+    uint8_t *h_buf = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(total, 1)));
+    int64_t *h_off = static_cast<int64_t *>(malloc(((size_t)n + 1) * 8));
+    if (!h_buf || !h_off) { free(h_buf); free(h_off); set_err("out of host memory"); return BSQ_E_NOMEM; }
+    hipError_t e = total ? hipMemcpyAsync(h_buf, d_buf, (size_t)total, hipMemcpyDeviceToHost, st) : hipSuccess;
+    if (e == hipSuccess) e = hipMemcpyAsync(h_off, d_off, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { free(h_buf); free(h_off); set_err("download: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
+    *buf = h_buf;
+    *offs = h_off;
+    return BSQ_OK;
+}
+
 extern "C" int bsq_nuclseq_encode_batch(int device, const char *text, const int64_t *offs, int64_t n, int validate,
                                         uint8_t **out, int64_t **out_off)
 {
@@ -1749,74 +1848,70 @@ extern "C" int bsq_nuclseq_encode_batch(int device, const char *text, const int6
     OwnStream os;
     HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
     hipStream_t st = os.s;
-    const int64_t T = toff[(size_t)n], slots = poff[(size_t)n], ntiles = (slots + 255) / 256;
-    if (ntiles + 1 >= INT32_MAX) { set_err("batch too large (%lld pac bytes)", (long long)slots); return BSQ_E_INVALID; }
     DevAllocs da;
-    uint8_t *d_text, *d_out;
-    int64_t *d_toff, *d_poff, *tile_hb, *tile_hs, *hb_base, *hs_base, *d_off;
-    uint32_t *loc;
-    unsigned long long *bad;
-    HIPCHK(da.get(d_text, (size_t)T));
-    HIPCHK(da.get(d_toff, (size_t)n + 1));
-    HIPCHK(da.get(d_poff, (size_t)n + 1));
-    HIPCHK(da.get(tile_hb, (size_t)ntiles + 1));
-    HIPCHK(da.get(tile_hs, (size_t)ntiles + 1));
-    HIPCHK(da.get(hb_base, (size_t)n + 1));
-    HIPCHK(da.get(hs_base, (size_t)n + 1));
-    HIPCHK(da.get(d_off, (size_t)n + 1));
-    HIPCHK(da.get(loc, (size_t)n + 1));
-    HIPCHK(da.get(bad, 1));
-    if (T) HIPCHK(hipMemcpyAsync(d_text, text + offs[0], (size_t)T, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(tile_hb, 0, ((size_t)ntiles + 1) * 8, st));
-    HIPCHK(hipMemsetAsync(tile_hs, 0, ((size_t)ntiles + 1) * 8, st));
-    HIPCHK(hipMemsetAsync(bad, 0xff, 8, st));
-    hipEvent_t ev[4];
-    for (auto &e : ev) HIPCHK(hipEventCreate(&e));
-    struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 4; ++i) hipEventDestroy(e[i]); } } evf{ev};
-    const EncView v{d_text, d_toff, d_poff, n, slots, validate ? 1 : 0};
-    HIPCHK(hipEventRecord(ev[0], st));
-    HIPCHK(launch_enc_count(st, v, ntiles, tile_hb, tile_hs, loc, bad));
-    size_t tb = 0, tb2 = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, d_off, d_off, (int)(n + 1), st));
-    uint8_t *cub = nullptr;
-    HIPCHK(da.get(cub, std::max(tb, tb2)));
-    tb = std::max(tb, tb2);
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, tile_hs, tile_hs, (int)(ntiles + 1), st));
-    HIPCHK(launch_enc_meta(st, v, tile_hb, tile_hs, ntiles, loc, hb_base, hs_base, d_off));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_off, d_off, (int)(n + 1), st));
-    int64_t tot[2] = {0, 0};
+    uint8_t *d_text;
+    HIPCHK(da.get(d_text, (size_t)toff[(size_t)n]));
+    if (toff[(size_t)n]) HIPCHK(hipMemcpyAsync(d_text, text + offs[0], (size_t)toff[(size_t)n], hipMemcpyHostToDevice, st));
+    uint8_t *d_out = nullptr;
+    int64_t *d_off = nullptr, total = 0;
     unsigned long long first_bad = ~0ull;
-    HIPCHK(hipEventRecord(ev[1], st));
-    HIPCHK(hipMemcpyAsync(&tot[0], d_off + n, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&tot[1], hs_base + n, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    double kms = 0;
+    { const int rc = encode_device(st, da, d_text, toff, poff, n, validate != 0, &d_out, &d_off, &total, &first_bad, &kms);
+      if (rc) return rc; }
     if (validate && first_bad != ~0ull) {   // the first text (in order) with a character nuclseq_in rejects
         set_err("invalid nucleotide in nuclseq_in: '%c'", text[offs[0] + (int64_t)first_bad]);
         return BSQ_E_INVALID;
     }
-    HIPCHK(da.get(d_out, (size_t)tot[0]));
-    HIPCHK(hipEventRecord(ev[2], st));
-    HIPCHK(launch_enc_write(st, v, ntiles, tile_hb, tile_hs, hb_base, hs_base, d_off, tot[1], d_out));
-    HIPCHK(hipEventRecord(ev[3], st));
-    uint8_t *h_out = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(tot[0], 1)));
-    int64_t *h_off = static_cast<int64_t *>(malloc(((size_t)n + 1) * 8));
-    if (!h_out || !h_off) { free(h_out); free(h_off); set_err("out of host memory"); return BSQ_E_NOMEM; }
-    hipError_t e = hipMemcpyAsync(h_out, d_out, (size_t)tot[0], hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_off, d_off, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) { free(h_out); free(h_off); set_err("encode: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
-    float a = 0, b = 0;
-    hipEventElapsedTime(&a, ev[0], ev[1]);
-    hipEventElapsedTime(&b, ev[2], ev[3]);
-    g_codec_ms[0] = a + b;
+    { const int rc = download(st, d_out, d_off, n, total, out, out_off); if (rc) return rc; }
+    g_codec_ms[0] = kms;
     g_codec_ms[1] = now_ms() - t_call;
-    *out = h_out;
-    *out_off = h_off;
+    return BSQ_OK;
+}
+
+// build_tuple_bwa's two nuclseq columns for every row of the last run (extension.cpp:282-305, which calls
+// nuclseq_from_text on ref_subseq and query_subseq per row, :285,290): the subsequence texts are written
+// by the GPU renderer and encoded in place by the bulk codec; varlena 2k = ref_subseq of row k, 2k+1 =
+// its query_subseq.
+extern "C" int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **out, int64_t **out_off)
+{
+    if (!b || !out || !out_off) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *out = nullptr; *out_off = nullptr;
+    const double t_call = now_ms();
+    const bsq_hits &H = b->view;
+    const int64_t n = 2 * H.n_hits;
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t st = b->stream;
+    std::vector<int64_t> toff((size_t)n + 1, 0), poff((size_t)n + 1, 0);
+    for (int64_t k = 0; k < H.n_hits; ++k) {
+        const bsq_hit &x = H.hits[k];
+        const int64_t l[2] = {x.re - x.rb, (int64_t)x.qe - x.qb};
+        for (int t = 0; t < 2; ++t) {
+            const size_t i = (size_t)(2 * k + t);
+            toff[i + 1] = toff[i] + l[t];
+            poff[i + 1] = poff[i] + (l[t] + 3) / 4;
+        }
+    }
+    DevAllocs da;
+    char *d_text;
+    int64_t *d_toff;
+    HIPCHK(da.get(d_text, (size_t)toff[(size_t)n]));
+    HIPCHK(da.get(d_toff, (size_t)n + 1));
+    RenderInputs ri;
+    if (H.n_hits) {
+        { const int rc = render_inputs(b, reads, ri); if (rc) return rc; }
+        HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_sub_write(st, ri.v, d_toff, d_text));
+    }
+    uint8_t *d_out = nullptr;
+    int64_t *d_off = nullptr, total = 0;
+    unsigned long long first_bad = ~0ull;
+    double kms = 0;
+    { const int rc = encode_device(st, da, reinterpret_cast<const uint8_t *>(d_text), toff, poff, n, false, &d_out, &d_off,
+                                   &total, &first_bad, &kms);
+      if (rc) return rc; }
+    { const int rc = download(st, d_out, d_off, n, total, out, out_off); if (rc) return rc; }
+    g_codec_ms[0] = kms;
+    g_codec_ms[1] = now_ms() - t_call;
     return BSQ_OK;
 }
 

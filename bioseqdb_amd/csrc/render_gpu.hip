@@ -70,58 +70,68 @@ __global__ void k_row_len(RenderView v, int64_t *len)
 
 DEV int pac_base(const uint8_t *pac, int64_t i) { return (pac[i >> 2] >> ((~i & 3) << 1)) & 3; }
 
+// ref_subseq of one row at o; returns the end
+DEV char *ref_subseq(const RenderView &v, const bsq_hit &x, char *o)
+{
+    char *s = o;
+    const int64_t rb = x.rb, re = x.re;
+    if (rb < v.l_pac) {
+        for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[pac_base(v.pac, i)];
+        if (v.n_holes) {   // holes with beg in (rb - hole_max, re), applied in their original order
+            int lo = 0, hi = v.n_holes;
+            const int64_t from = rb - v.hole_max;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (v.holes[mid].beg < from) lo = mid + 1; else hi = mid; }
+            uint32_t done = 0;   // apply by increasing order: repeatedly the smallest order above `done`
+            for (;;) {
+                uint32_t best = 0xffffffffu;
+                int bi = -1;
+                for (int h = lo; h < v.n_holes && v.holes[h].beg < re; ++h) {
+                    const RenderHole &H = v.holes[h];
+                    if (H.end <= rb || H.order + 1 <= done) continue;
+                    if (H.order < best) { best = H.order; bi = h; }
+                }
+                if (bi < 0) break;
+                const RenderHole &H = v.holes[bi];
+                const int64_t a = H.beg > rb ? H.beg : rb, b = H.end < re ? H.end : re;
+                for (int64_t i = a; i < b; ++i) s[i - rb] = (char)H.amb;
+                done = H.order + 1;
+            }
+        }
+    } else {   // Q7: the reverse-strand reference text
+        for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[3 - pac_base(v.pac, (v.l_pac << 1) - 1 - i)];
+    }
+    return o;
+}
+
+// query_subseq of one row at o: the read's text (ns_to_text) over [qb, qe); returns the end
+DEV char *query_subseq(const RenderView &v, const bsq_hit &x, char *o)
+{
+    const uint8_t *q = v.codes + v.offs[x.read_index];
+    char *s = o;
+    for (int j = x.qb; j < x.qe; ++j) { const int c = q[j]; *o++ = c < 4 ? "ACGT"[c] : 'N'; }
+    if (v.rh_off) {
+        const int64_t h0 = v.rh_off[x.read_index], h1 = v.rh_off[x.read_index + 1];
+        for (int64_t h = h0; h < h1; ++h) {   // in the nuclseq's order: later holes win
+            const RenderHole &H = v.rh[h];
+            const int64_t a = H.beg > x.qb ? H.beg : x.qb, b = H.end < x.qe ? H.end : x.qe;
+            for (int64_t i = a; i < b; ++i) s[i - x.qb] = (char)H.amb;
+        }
+    }
+    return o;
+}
+
 __global__ void k_row_write(RenderView v, const int64_t *off, char *out)
 {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < v.n_hits; k += (int64_t)gridDim.x * blockDim.x) {
         const bsq_hit x = v.hits[k];
         char *o = out + off[k];
         o = put_int(o, x.ref_id); *o++ = '\t';
-        {   // ref_subseq
-            char *s = o;
-            const int64_t rb = x.rb, re = x.re;
-            if (rb < v.l_pac) {
-                for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[pac_base(v.pac, i)];
-                if (v.n_holes) {   // holes with beg in (rb - hole_max, re), applied in their original order
-                    int lo = 0, hi = v.n_holes;
-                    const int64_t from = rb - v.hole_max;
-                    while (lo < hi) { const int mid = (lo + hi) >> 1; if (v.holes[mid].beg < from) lo = mid + 1; else hi = mid; }
-                    uint32_t done = 0;   // apply by increasing order: repeatedly the smallest order above `done`
-                    for (;;) {
-                        uint32_t best = 0xffffffffu;
-                        int bi = -1;
-                        for (int h = lo; h < v.n_holes && v.holes[h].beg < re; ++h) {
-                            const RenderHole &H = v.holes[h];
-                            if (H.end <= rb || H.order + 1 <= done) continue;
-                            if (H.order < best) { best = H.order; bi = h; }
-                        }
-                        if (bi < 0) break;
-                        const RenderHole &H = v.holes[bi];
-                        const int64_t a = H.beg > rb ? H.beg : rb, b = H.end < re ? H.end : re;
-                        for (int64_t i = a; i < b; ++i) s[i - rb] = (char)H.amb;
-                        done = H.order + 1;
-                    }
-                }
-            } else {   // Q7: the reverse-strand reference text
-                for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[3 - pac_base(v.pac, (v.l_pac << 1) - 1 - i)];
-            }
-        }
+        o = ref_subseq(v, x, o);
         *o++ = '\t';
         o = put_int(o, x.ref_match_start); *o++ = '\t';
         o = put_int(o, x.ref_match_end); *o++ = '\t';
         o = put_int(o, x.ref_match_len); *o++ = '\t';
-        {   // query_subseq: the read's text (ns_to_text) over [qb, qe)
-            const uint8_t *q = v.codes + v.offs[x.read_index];
-            char *s = o;
-            for (int j = x.qb; j < x.qe; ++j) { const int c = q[j]; *o++ = c < 4 ? "ACGT"[c] : 'N'; }
-            if (v.rh_off) {
-                const int64_t h0 = v.rh_off[x.read_index], h1 = v.rh_off[x.read_index + 1];
-                for (int64_t h = h0; h < h1; ++h) {   // in the nuclseq's order: later holes win
-                    const RenderHole &H = v.rh[h];
-                    const int64_t a = H.beg > x.qb ? H.beg : x.qb, b = H.end < x.qe ? H.end : x.qe;
-                    for (int64_t i = a; i < b; ++i) s[i - x.qb] = (char)H.amb;
-                }
-            }
-        }
+        o = query_subseq(v, x, o);
         *o++ = '\t';
         o = put_int(o, x.qb); *o++ = '\t';
         o = put_int(o, x.qe); *o++ = '\t';
@@ -140,6 +150,17 @@ __global__ void k_row_write(RenderView v, const int64_t *off, char *out)
     }
 }
 
+// the two subsequence texts of every row (build_tuple_bwa's nuclseq_from_text inputs, extension.cpp:285,290):
+// text 2k = ref_subseq of row k, text 2k+1 = its query_subseq, at toff[]
+__global__ void k_sub_write(RenderView v, const int64_t *toff, char *out)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < v.n_hits; k += (int64_t)gridDim.x * blockDim.x) {
+        const bsq_hit x = v.hits[k];
+        ref_subseq(v, x, out + toff[2 * k]);
+        query_subseq(v, x, out + toff[2 * k + 1]);
+    }
+}
+
 inline dim3 rgrid(int64_t n) { const int64_t b = (n + 255) / 256; return dim3((unsigned)(b < 65536 ? (b ? b : 1) : 65536)); }
 
 hipError_t launch_row_len(hipStream_t st, const RenderView &v, int64_t *len)
@@ -151,6 +172,12 @@ hipError_t launch_row_len(hipStream_t st, const RenderView &v, int64_t *len)
 hipError_t launch_row_write(hipStream_t st, const RenderView &v, const int64_t *off, char *out)
 {
     hipLaunchKernelGGL(k_row_write, rgrid(v.n_hits), dim3(256), 0, st, v, off, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sub_write(hipStream_t st, const RenderView &v, const int64_t *toff, char *out)
+{
+    hipLaunchKernelGGL(k_sub_write, rgrid(v.n_hits), dim3(256), 0, st, v, toff, out);
     return hipGetLastError();
 }
 

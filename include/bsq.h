@@ -202,6 +202,11 @@ int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const uint64_t *
  * holes (NULL: ambiguous bases print as N).  *text is borrowed (NUL-terminated, *len bytes), valid until
  * the next run, render or free of the batch. */
 int bsq_batch_render(bsq_batch *b, const void *const *reads, const char **text, int64_t *len);
+/* build_tuple_bwa's nuclseq columns of the last run's rows on the GPU (extension.cpp:282-305; per row it calls
+ * nuclseq_from_text on ref_subseq and query_subseq, :285,290): varlena 2k = ref_subseq of row k, 2k+1 = its
+ * query_subseq, the same bytes nuclseq_from_text gives for the texts bsq_render_tsv prints.  Layout as
+ * bsq_nuclseq_encode_batch; both outputs malloc'd (bsq_free). */
+int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **out, int64_t **out_off);
 /* Runs n batches concurrently (one host thread and HIP stream each); batch i draws lrand48 values from
  * first_call[i].  Each batch keeps its own result view.  Returns the first error, prefixed by the batch
  * index. */

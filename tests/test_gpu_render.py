@@ -1,6 +1,7 @@
 """bwa_result rows rendered on the GPU (bsq_batch_render) are byte-identical to
 the host renderer (bsq_render_tsv): reference rows with N/IUPAC runs (Q3 overlay), reverse-strand rows
-(Q7), clips printed as N (Q8), reads with IUPAC symbols, multi-chunk batches."""
+(Q7), clips printed as N (Q8), reads with IUPAC symbols, multi-chunk batches; and the rows' two nuclseq
+columns (bsq_batch_render_nuclseqs) equal nuclseq_from_text of the printed subsequences."""
 import ctypes
 import random
 
@@ -62,5 +63,19 @@ def test_gpu_render_matches_host(monkeypatch, chunk):
         assert n.value == len(host) and host.count(b"\n") >= 2000
         assert gpu == host
         assert b"\tf\tf\tt\t" in gpu or b"\tt\tf\tt\t" in gpu   # reverse-strand rows present
+        # build_tuple_bwa's nuclseq columns (bsq_batch_render_nuclseqs) = nuclseq_from_text of the printed texts
+        out, oo = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(L.bsq_batch_render_nuclseqs(b, arr, ctypes.byref(out), ctypes.byref(oo)))
+        rows = host.decode().splitlines()
+        off = np.ctypeslib.as_array(ctypes.cast(oo, ctypes.POINTER(ctypes.c_int64)), shape=(2 * len(rows) + 1,)).copy()
+        raw = ctypes.string_at(out, int(off[-1]))
+        L.bsq_free(out)
+        L.bsq_free(oo)
+        for k, row in enumerate(rows):
+            f = row.split("\t")
+            for t, col in ((0, 1), (1, 5)):
+                a0 = int(off[2 * k + t])
+                size = int.from_bytes(raw[a0:a0 + 4], "little") >> 2
+                assert raw[a0:a0 + size] == NucleotideSequence._encode(f[col]).raw, (k, col)
     finally:
         L.bsq_batch_free(b)
