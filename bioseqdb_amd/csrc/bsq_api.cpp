@@ -168,6 +168,7 @@ extern "C" int bsq_index_create(bsq_index **out)
 extern "C" void bsq_index_free(bsq_index *idx)
 {
     if (!idx) return;
+    bsq_batch_free(idx->pool);
     delete idx->h.dev;
     delete idx;
 }
@@ -1670,11 +1671,26 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
         return BSQ_OK;
     }
     if (!idx->h.dev) { free(h); set_err("index not uploaded to a device (call bsq_index_upload)"); return BSQ_E_NODEV; }
+    // the index's pooled batch when it is free and large enough (its workspace is reused across calls)
     bsq_batch *b = nullptr;
-    int rc = bsq_batch_create(idx, n_reads, n_bases, &b);
+    int rc = BSQ_OK;
+    std::unique_lock<std::mutex> lk(idx->pool_mu, std::try_to_lock);
+    const bool pooled = lk.owns_lock();
+    if (pooled) {
+        if (idx->pool && (idx->pool->max_reads < n_reads || idx->pool->max_bases < n_bases)) {
+            bsq_batch_free(idx->pool);
+            idx->pool = nullptr;
+        }
+        if (!idx->pool) rc = bsq_batch_create(idx, n_reads, n_bases, &idx->pool);
+        b = idx->pool;
+    } else rc = bsq_batch_create(idx, n_reads, n_bases, &b);
     if (rc == BSQ_OK) rc = bsq_batch_set_nuclseqs(b, reads, n_reads);
     if (rc == BSQ_OK) rc = bsq_batch_run(b, opts, first_call_seq);
-    if (rc != BSQ_OK) { bsq_batch_free(b); free(h); return rc; }
+    if (rc != BSQ_OK) {
+        if (pooled) { bsq_batch_free(idx->pool); idx->pool = nullptr; } else bsq_batch_free(b);
+        free(h);
+        return rc;
+    }
     h->n_hits = b->view.n_hits;
     h->n_cigar = b->view.n_cigar;
     h->hits = (bsq_hit *)malloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
@@ -1683,7 +1699,7 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     memcpy(h->hits, b->view.hits, sizeof(bsq_hit) * (size_t)h->n_hits);
     memcpy(h->cigar, b->view.cigar, 4 * (size_t)h->n_cigar);
     memcpy(h->read_off, b->view.read_off, 8 * ((size_t)n_reads + 1));
-    bsq_batch_free(b);
+    if (!pooled) bsq_batch_free(b);
     *out = h;
     return BSQ_OK;
 }

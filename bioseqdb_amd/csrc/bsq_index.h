@@ -3,6 +3,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -69,4 +70,11 @@ struct HostIndex {
 }  // namespace bsq
 
 // opaque C-ABI handle (include/bsq.h)
-struct bsq_index { bsq::HostIndex h; };
+struct bsq_batch;
+// the index plus one reusable batch for the one-shot bsq_align_batch (its workspace survives across calls;
+// a concurrent caller that finds it busy uses a batch of its own)
+struct bsq_index {
+    bsq::HostIndex h;
+    std::mutex pool_mu;
+    bsq_batch *pool = nullptr;
+};
