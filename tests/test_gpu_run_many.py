@@ -60,3 +60,28 @@ def test_run_many_equals_one_batch(S):
         L.bsq_batch_free(whole)
         for b in subs:
             L.bsq_batch_free(b)
+
+
+def test_one_shot_calls_concurrent_and_repeated():
+    """bsq_align_batch from several host threads on one index (one takes the index's pooled batch, the
+    others batches of their own) and repeated calls of different sizes give the same rows."""
+    import threading
+    from bioseqdb_amd import NucleotideSequence
+    ref = synth.make_reference(500_000, n_rows=1, n_run_every=200_000, n_run_len=300)
+    reads = synth.make_reads(ref, 3000, seed=43)
+    pi, _ = build_pair([t.decode() for t in ref.texts()])
+    seqs = [NucleotideSequence.from_text(reads.text(i)) for i in range(reads.n)]
+    exp = pi.align_sequences(seqs, pi.options, first_call=0)
+    assert pi.align_sequences(seqs[:10], pi.options, first_call=0) == exp[:10]   # smaller call, pooled batch
+    assert pi.align_sequences(seqs, pi.options, first_call=0) == exp             # and back to the full size
+    got = [None] * 4
+
+    def run(k):
+        got[k] = pi.align_sequences(seqs, pi.options, first_call=0)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert all(g == exp for g in got)
