@@ -391,6 +391,25 @@ def main() -> int:
     di = names.index(dom)
     achieved = stage_bytes[di] / (stage_ms[di] * 1e-3) / 1e9 if stage_ms[di] > 0 else 0.0
 
+    # the dominant stage once more as a lone launch over all the reads (one batch, nothing sharing the CUs),
+    # outside the timed region: the kernel's own roofline beside the shared-CU figure of the timed run
+    iso = None
+    if world == 1 and S > 1 and not cfg["seeding"]:
+        hb.phase = "isolated single-batch launch"
+        wb = ctypes.c_void_p()
+        N.check(L.bsq_batch_create(idx, reads.n, int(reads.offsets[-1]), ctypes.byref(wb)))
+        try:
+            N.check(L.bsq_batch_set_reads(wb, codes.ctypes.data, offs.ctypes.data, reads.n))
+            for _ in range(2):   # warm-up + measured
+                N.check(L.bsq_batch_run(wb, ctypes.byref(opts), first_call))
+            ms = (ctypes.c_float * 6)()
+            L.bsq_batch_stage_ms(wb, ms, 6)
+            by = (ctypes.c_double * 6)()
+            L.bsq_batch_stage_bytes(wb, by, 6)
+            iso = (float(ms[di]), float(by[di]))
+        finally:
+            L.bsq_batch_free(wb)
+
     total_reads = args.reads * world
     value = total_reads * args.steps / elapsed
     result = {
@@ -632,6 +651,12 @@ def main() -> int:
                                         "per reference window, + the packed read)")
             rf["achieved"] = round(alg / (rf["launch_ms"] * 1e-3) / 1e9, 2)
             rf["frac"] = round(rf["achieved"] / HBM_PEAK_GBS, 5)
+            if iso:
+                a_iso = per_read[ki] * reads.n / (iso[0] * 1e-3) / 1e9
+                rf["isolated"] = {"reads_per_launch": reads.n, "launch_ms": round(iso[0], 3),
+                                  "achieved": round(a_iso, 2), "frac": round(a_iso / HBM_PEAK_GBS, 5),
+                                  "issued_gbs": round(iso[1] / (iso[0] * 1e-3) / 1e9, 2),
+                                  "note": "one untimed launch over all reads with nothing else on the GPU"}
         for i, nm in enumerate(names[:1 if cfg["seeding"] else 4]):
             k = result["kernels"][STAGE_KERNEL[nm]]
             k["algorithmic_bytes_8d"] = per_read[i] * reads_per_launch
