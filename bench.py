@@ -233,6 +233,11 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-codec", action="store_true", help="skip the bulk nuclseq codec measurement")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the untimed lone launch of the dominant stage")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="only the timed steps (profiling passes): no CPU baseline, codec, isolated launch, rendering "
+                         "or one-shot call, so every dispatch of a stage kernel is a timed-step launch")
     ap.add_argument("--streams", type=int, default=4,
                     help="concurrent batches per GPU (bsq_batch_run_many); each aligns 1/S of the reads")
     ap.add_argument("--index-build", default="device", choices=["device", "host"],
@@ -240,6 +245,8 @@ def main() -> int:
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
+    if args.timed_only:
+        args.no_cpu_baseline = args.no_codec = args.no_isolated = True
     cfg = CONFIGS[args.config]
     args.reads = args.reads or cfg["reads"]
     args.ref_bp = args.ref_bp or cfg["ref_bp"]
@@ -400,7 +407,7 @@ def main() -> int:
     # the dominant stage once more as a lone launch over all the reads (one batch, nothing sharing the CUs),
     # outside the timed region: the kernel's own roofline beside the shared-CU figure of the timed run
     iso = None
-    if world == 1 and S > 1 and not cfg["seeding"]:
+    if world == 1 and S > 1 and not cfg["seeding"] and not args.no_isolated:
         hb.phase = "isolated single-batch launch"
         wb = ctypes.c_void_p()
         N.check(L.bsq_batch_create(idx, reads.n, int(reads.offsets[-1]), ctypes.byref(wb)))
@@ -465,7 +472,7 @@ def main() -> int:
     }
 
     # ---- host materialisation: the last step's rows rendered as bwa_result text ----
-    if rank == 0 and not cfg["seeding"] and n_hits:
+    if rank == 0 and not cfg["seeding"] and n_hits and not args.timed_only:
         hb.phase = "rendering rows on the host"
         keep, ptrs = reads_as_nuclseq(L, reads)
         base = ctypes.addressof(ptrs)
