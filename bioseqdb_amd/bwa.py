@@ -17,6 +17,7 @@ import ctypes
 import dataclasses
 import hashlib
 import os
+import re
 import struct
 from collections import OrderedDict
 from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
@@ -25,6 +26,7 @@ from . import _native
 from ._native import BsqError, Opts, check, lib
 
 ALLOWED_NUCLEOTIDES = "ACGTNWSMKRYBDHV"   # sequence.h:46
+_INVALID_NUCLEOTIDE = re.compile(f"[^{ALLOWED_NUCLEOTIDES}]", re.S)
 
 
 class InvalidTextRepresentation(ValueError):
@@ -53,9 +55,9 @@ class NucleotideSequence:
         """nuclseq_in (extension.cpp:46-61): validates the alphabet then nuclseq_from_text."""
         if len(text) > 0x7FFFFFFF // 4:
             raise InvalidParameterValue("provided sequence is too long")
-        for ch in text:
-            if ch not in ALLOWED_NUCLEOTIDES:
-                raise InvalidTextRepresentation(f"invalid nucleotide in nuclseq_in: '{ch}'")
+        bad = _INVALID_NUCLEOTIDE.search(text)
+        if bad:
+            raise InvalidTextRepresentation(f"invalid nucleotide in nuclseq_in: '{bad.group(0)}'")
         return cls._encode(text)
 
     @classmethod

@@ -1680,8 +1680,16 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
                          uint8_t *scratch, Counters *ctr, const int32_t *order, const int32_t *sscore)
 {
     // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
-    static const bool force_g = getenv("BSQ_EXT") && getenv("BSQ_EXT")[0] == 'g';   // timing experiments only
-    const bool lds = !force_g && cp.max_len <= 200 &&
+    // and the 64-column ring holds the band: ksw_extend2 clamps w to max_ins/max_del (ksw.c), which for
+    // cheap gap extensions (e.g. e_del = 1) leaves bands up to 2w+1 = 201 columns wide.  The retry pass
+    // (sel != nullptr) always takes the global-row kernel, so a read whose window outgrew the ring
+    // completes there.
+    const int end_bonus = o.pen_clip3 > o.pen_clip5 ? o.pen_clip3 : o.pen_clip5;
+    const int mx = o.mat_max > 0 ? o.mat_max : 0;
+    int wb = o.w;
+    wb = std::min(wb, std::max(1, (int)((double)(cp.max_len * mx + end_bonus - o.o_ins) / o.e_ins + 1.)));
+    wb = std::min(wb, std::max(1, (int)((double)(cp.max_len * mx + end_bonus - o.o_del) / o.e_del + 1.)));
+    const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 &&
                      (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
         static const size_t sh_env = getenv("BSQ_EXT_SH") ? (size_t)atol(getenv("BSQ_EXT_SH")) : 0;   // tuning only

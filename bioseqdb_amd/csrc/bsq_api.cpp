@@ -622,6 +622,8 @@ __global__ void k_lrand_ids(uint64_t first, int n, int64_t *ids)
 // ================================================================================================
 namespace {
 
+constexpr int N_RETRY_LEVELS = 3;   // retry workspaces per batch (retry_caps)
+
 struct Workspace {
     Caps cp{};
     int32_t max_reads = 0;
@@ -699,7 +701,10 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     HIPCHK(hipMalloc(&w.regs, R * cp.regs * sizeof(Reg)));
     HIPCHK(hipMalloc(&w.hits, R * cp.regs * sizeof(Hit)));
     HIPCHK(hipMalloc(&w.cigars, R * cp.regs * cp.cigar * 4));
-    w.scratch_total = (int64_t)w.grid * 256 * w.cp.scratch;
+    // Every stage kernel derives its scratch pointer from the thread id but dereferences it only inside
+    // `for (li = tid; li < n; ...)`; a retry workspace runs n <= max_reads reads per launch, so only
+    // max_reads threads ever touch scratch (the main pass may run more reads than threads: full grid).
+    w.scratch_total = (with_sel ? (int64_t)std::max(max_reads, 1) : (int64_t)w.grid * 256) * w.cp.scratch;
     HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
     if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
     if (long_reads(cp.max_len)) HIPCHK(hipMalloc(&w.sscore, R * cp.seeds * 4));
@@ -758,7 +763,7 @@ struct bsq_batch {
     int64_t ns_dev_cap = 0;
     int64_t *ns_meta = nullptr;   // in_off | poff | holed texts
     int64_t ns_meta_cap = 0;
-    Workspace main, retry;
+    Workspace main, retry[N_RETRY_LEVELS];
     Counters *ctr = nullptr;
     // packing
     int64_t *cnt_hits = nullptr, *cnt_cig = nullptr, *off_hits = nullptr, *off_cig = nullptr;
@@ -823,15 +828,22 @@ static Caps main_caps(int max_len)
     return c;
 }
 
-static Caps retry_caps(int max_len)
+// Retry levels: a read that overflows the main pass is re-run at level 0 (256 reads per launch); one that
+// overflows that too (e.g. min_seed_len = 0 with a large max_occ expands thousands of SA hits per read) at
+// level 1 and then level 2, each with ~8x the per-read capacities and 1/16 the reads per launch.  libbwa's
+// own vectors are unbounded; only a read beyond level 2 fails (BSQ_E_UNSUPPORTED).
+static int retry_chunk(int level) { return 256 >> (4 * level); }            // 256, 16, 1 reads
+static int64_t retry_zcap(int level) { return (int64_t)(4 << 20) << (2 * level); }   // 4, 16, 64 MB traceback
+static Caps retry_caps(int max_len, int level)
 {
     Caps c{};
+    const int f = 1 << (3 * level);
     c.max_len = max_len;
-    c.intv = 4 * max_len + 64;
-    c.seeds = 32768;
-    c.chains = 32768;
-    c.regs = 2048;
-    c.cigar = 2 * max_len + 8;
+    c.intv = (4 * max_len + 64) * f;
+    c.seeds = 32768 * f;
+    c.chains = 32768 * f;
+    c.regs = 2048 << (2 * level);
+    c.cigar = (2 * max_len + 8) * (1 + level);
     return c;
 }
 
@@ -886,7 +898,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipSetDevice(b->device);
     if (b->stream) hipStreamSynchronize(b->stream);
     b->main.release();
-    b->retry.release();
+    for (auto &r : b->retry) r.release();
     hipFree(b->codes); hipFree(b->offs); hipFree(b->ids); hipFree(b->ctr);
     hipFree(b->cnt_hits); hipFree(b->cnt_cig); hipFree(b->off_hits); hipFree(b->off_cig); hipFree(b->unresolved);
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
@@ -1146,11 +1158,11 @@ static int pack_main(bsq_batch *b, Workspace &w, int n, int lo, int64_t hit_dst,
 
 // Retry-pass chunk: records (chunk-local indices) into host vectors.
 static int pack_retry(bsq_batch *b, Workspace &w, int n, std::vector<bsq_hit> &hits, std::vector<uint32_t> &cig,
-                      std::vector<int64_t> &off)
+                      std::vector<int64_t> &off, bool last_level)
 {
     hipStream_t st = b->stream;
     int64_t tot[2];
-    { const int rc = pack_device(b, w, n, false, 0, 0, tot); if (rc) return rc; }
+    { const int rc = pack_device(b, w, n, !last_level, 0, 0, tot); if (rc) return rc; }
     off.resize((size_t)n + 1);
     hits.resize((size_t)tot[0]);
     cig.resize((size_t)tot[1]);
@@ -1159,6 +1171,16 @@ static int pack_retry(bsq_batch *b, Workspace &w, int n, std::vector<bsq_hit> &h
     if (tot[1]) HIPCHK(hipMemcpyAsync(cig.data(), b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return BSQ_OK;
+}
+
+// The retry workspace of `level`, (re)allocated for the batch's longest read.
+static int ensure_retry(bsq_batch *b, int level)
+{
+    Workspace &r = b->retry[level];
+    if (r.status && r.cp.max_len >= b->max_len) return BSQ_OK;
+    r.release();
+    const int ch = retry_chunk(level);
+    return ws_alloc(r, retry_caps(std::max(b->max_len, 1), level), ch, ch, retry_zcap(level), true);
 }
 
 // One workspace pass over reads [b->lo, b->lo + n): main pass, packing into the batch-wide pinned arrays
@@ -1194,34 +1216,44 @@ static int run_chunk(bsq_batch *b, const DOpts &o, int n, int64_t &hit_total, in
     std::vector<int32_t> list((size_t)novf);
     HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
     std::sort(list.begin(), list.end());
-    const int CH = 256;
-    if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
-        b->retry.release();
-        rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
-        if (rc) return rc;
-    }
-    // per-read replacement results
+    // per-read replacement results, escalating through the retry levels
     std::vector<std::vector<bsq_hit>> rh((size_t)novf);
     std::vector<std::vector<uint32_t>> rcg((size_t)novf);
-    for (int s = 0; s < novf; s += CH) {
-        int m = std::min(CH, novf - s);
-        HIPCHK(hipMemcpyAsync(b->retry.sel, list.data() + s, (size_t)m * 4, hipMemcpyHostToDevice, st));
-        rc = run_stages(b, b->retry, o, m, b->retry.sel, false);
+    std::vector<int32_t> pend((size_t)novf);   // positions in `list` still unresolved
+    for (int k = 0; k < novf; ++k) pend[(size_t)k] = k;
+    for (int level = 0; level < N_RETRY_LEVELS && !pend.empty(); ++level) {
+        rc = ensure_retry(b, level);
         if (rc) return rc;
-        std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
-        rc = pack_retry(b, b->retry, m, hh, cc, oo);
-        if (rc) return rc;
-        for (int j = 0; j < m; ++j) {
-            auto &dst = rh[(size_t)(s + j)];
-            auto &dc = rcg[(size_t)(s + j)];
-            for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
-                bsq_hit x = hh[(size_t)k];
-                uint32_t base = (uint32_t)dc.size();
-                dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
-                x.cigar_off = base;
-                dst.push_back(x);
+        Workspace &W = b->retry[level];
+        const int CH = retry_chunk(level);
+        const bool last = level + 1 == N_RETRY_LEVELS;
+        std::vector<int32_t> next, sel((size_t)CH);
+        std::vector<uint32_t> stt((size_t)CH);
+        for (size_t s = 0; s < pend.size(); s += (size_t)CH) {
+            const int m = (int)std::min<size_t>((size_t)CH, pend.size() - s);
+            for (int j = 0; j < m; ++j) sel[(size_t)j] = list[(size_t)pend[s + (size_t)j]];
+            HIPCHK(hipMemcpyAsync(W.sel, sel.data(), (size_t)m * 4, hipMemcpyHostToDevice, st));
+            rc = run_stages(b, W, o, m, W.sel, false);
+            if (rc) return rc;
+            std::vector<bsq_hit> hh; std::vector<uint32_t> cc; std::vector<int64_t> oo;
+            rc = pack_retry(b, W, m, hh, cc, oo, last);
+            if (rc) return rc;
+            HIPCHK(hipMemcpy(stt.data(), W.status, (size_t)m * 4, hipMemcpyDeviceToHost));
+            for (int j = 0; j < m; ++j) {
+                const int32_t li = pend[s + (size_t)j];
+                if (stt[(size_t)j] & ST_OVERFLOW) { next.push_back(li); continue; }
+                auto &dst = rh[(size_t)li];
+                auto &dc = rcg[(size_t)li];
+                for (int64_t k = oo[j]; k < oo[j + 1]; ++k) {
+                    bsq_hit x = hh[(size_t)k];
+                    uint32_t base = (uint32_t)dc.size();
+                    dc.insert(dc.end(), cc.begin() + x.cigar_off, cc.begin() + x.cigar_off + x.n_cigar);
+                    x.cigar_off = base;
+                    dst.push_back(x);
+                }
             }
         }
+        pend.swap(next);
     }
     // merge into read order (chunk-local): bulk copies of the runs of main-pass reads between retried ones
     std::vector<bsq_hit> &mh = b->res_hits;
@@ -1275,8 +1307,8 @@ static int run_chunk(bsq_batch *b, const DOpts &o, int n, int64_t &hit_total, in
 extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq)
 {
     if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
-    if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len <= 0) {
-        set_err("gap extension penalties, max_occ and min_seed_len must be positive");
+    if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len < 0) {
+        set_err("gap extension penalties and max_occ must be positive, min_seed_len nonnegative");
         return BSQ_E_INVALID;
     }
     HIPCHK(hipSetDevice(b->device));
@@ -1300,6 +1332,10 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
             rc = run_chunk(b, o, m, hit_total, cig_total);
             b->lo = 0;
             if (rc) return rc;
+            if (cig_total > (int64_t)UINT32_MAX) {   // bsq_hit.cigar_off is u32: offsets would wrap
+                set_err("batch holds more than 2^32 CIGAR operations; split it into smaller batches");
+                return BSQ_E_UNSUPPORTED;
+            }
         }
         // algorithmic bytes (stage times were summed over the chunks)
         Counters c[STG_N];
@@ -1352,35 +1388,44 @@ static int seed_chunk(bsq_batch *b, const DOpts &o, int n)
         std::vector<int32_t> list((size_t)novf);
         HIPCHK(hipMemcpy(list.data(), b->ovf_list, (size_t)novf * 4, hipMemcpyDeviceToHost));
         std::sort(list.begin(), list.end());
-        const int CH = 256;
-        if (!b->retry.status || b->retry.cp.max_len < b->max_len) {
-            b->retry.release();
-            const int rc = ws_alloc(b->retry, retry_caps(std::max(b->max_len, 1)), CH, CH, 4 << 20, true);
-            if (rc) return rc;
-        }
-        Workspace &r = b->retry;
-        std::vector<int32_t> cnt(CH);
-        std::vector<uint32_t> stt(CH);
-        std::vector<Intv> slots((size_t)CH * r.cp.intv);
-        for (int s0 = 0; s0 < novf; s0 += CH) {
-            const int m = std::min(CH, novf - s0);
-            HIPCHK(hipMemcpyAsync(r.sel, list.data() + s0, (size_t)m * 4, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemsetAsync(r.status, 0, (size_t)m * 4, st));
-            { const int rc = seed_stage(b, r, o, m, r.sel); if (rc) return rc; }
-            HIPCHK(hipMemcpyAsync(cnt.data(), r.n_intv, (size_t)m * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(stt.data(), r.status, (size_t)m * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(slots.data(), r.intv, (size_t)m * r.cp.intv * sizeof(Intv), hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            for (int j = 0; j < m; ++j) {
-                if (stt[j]) { set_err("read %d exceeded even the retry seeding capacities", b->lo + list[s0 + j]); return BSQ_E_UNSUPPORTED; }
-                std::vector<uint64_t> v((size_t)cnt[j] * 4);
-                for (int k = 0; k < cnt[j]; ++k) {
-                    const Intv &x = slots[(size_t)j * r.cp.intv + k];
-                    v[4 * k] = x.x[0]; v[4 * k + 1] = x.x[1]; v[4 * k + 2] = x.x[2]; v[4 * k + 3] = x.info;
+        std::vector<int32_t> pend = list;
+        for (int level = 0; level < N_RETRY_LEVELS && !pend.empty(); ++level) {
+            { const int rc = ensure_retry(b, level); if (rc) return rc; }
+            Workspace &r = b->retry[level];
+            const int CH = retry_chunk(level);
+            std::vector<int32_t> cnt((size_t)CH), next;
+            std::vector<uint32_t> stt((size_t)CH);
+            std::vector<Intv> slots((size_t)CH * r.cp.intv);
+            for (size_t s0 = 0; s0 < pend.size(); s0 += (size_t)CH) {
+                const int m = (int)std::min<size_t>((size_t)CH, pend.size() - s0);
+                HIPCHK(hipMemcpyAsync(r.sel, pend.data() + s0, (size_t)m * 4, hipMemcpyHostToDevice, st));
+                HIPCHK(hipMemsetAsync(r.status, 0, (size_t)m * 4, st));
+                { const int rc = seed_stage(b, r, o, m, r.sel); if (rc) return rc; }
+                HIPCHK(hipMemcpyAsync(cnt.data(), r.n_intv, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(stt.data(), r.status, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(slots.data(), r.intv, (size_t)m * r.cp.intv * sizeof(Intv), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                for (int j = 0; j < m; ++j) {
+                    if (stt[(size_t)j]) {
+                        if (level + 1 < N_RETRY_LEVELS) { next.push_back(pend[s0 + (size_t)j]); continue; }
+                        set_err("read %d exceeded even the retry seeding capacities", b->lo + pend[s0 + (size_t)j]);
+                        return BSQ_E_UNSUPPORTED;
+                    }
+                    std::vector<uint64_t> v((size_t)cnt[(size_t)j] * 4);
+                    for (int k = 0; k < cnt[(size_t)j]; ++k) {
+                        const Intv &x = slots[(size_t)j * r.cp.intv + k];
+                        v[4 * k] = x.x[0]; v[4 * k + 1] = x.x[1]; v[4 * k + 2] = x.x[2]; v[4 * k + 3] = x.info;
+                    }
+                    b->seed_retry.emplace_back(pend[s0 + (size_t)j], std::move(v));
                 }
-                b->seed_retry.emplace_back(list[s0 + j], std::move(v));
             }
+            pend.swap(next);
         }
+        // pack_seed_chunk merges seed_retry with the main slots in read order
+        std::sort(b->seed_retry.begin(), b->seed_retry.end(),
+                  [](const std::pair<int32_t, std::vector<uint64_t>> &x, const std::pair<int32_t, std::vector<uint64_t>> &y) {
+                      return x.first < y.first;
+                  });
     }
     float ms = 0;
     hipEventElapsedTime(&ms, b->ev[STG_SMEM], b->ev[STG_CHAIN]);
@@ -1426,7 +1471,10 @@ static int pack_seed_chunk(bsq_batch *b, int n)
 extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
 {
     if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
-    if (opts->max_occ <= 0 || opts->min_seed_len <= 0) { set_err("max_occ and min_seed_len must be positive"); return BSQ_E_INVALID; }
+    if (opts->max_occ <= 0 || opts->min_seed_len < 0) {
+        set_err("max_occ must be positive, min_seed_len nonnegative");
+        return BSQ_E_INVALID;
+    }
     HIPCHK(hipSetDevice(b->device));
     const int n = b->n_reads;
     const DOpts o = make_dopts(*opts);
@@ -1696,6 +1744,12 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     h->hits = (bsq_hit *)malloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
     h->cigar = (uint32_t *)malloc(4 * (size_t)std::max<int64_t>(h->n_cigar, 1));
     h->read_off = (int64_t *)malloc(8 * ((size_t)n_reads + 1));
+    if (!h->hits || !h->cigar || !h->read_off) {
+        if (!pooled) bsq_batch_free(b);
+        bsq_hits_free(h);
+        set_err("out of host memory for the hit records");
+        return BSQ_E_NOMEM;
+    }
     memcpy(h->hits, b->view.hits, sizeof(bsq_hit) * (size_t)h->n_hits);
     memcpy(h->cigar, b->view.cigar, 4 * (size_t)h->n_cigar);
     memcpy(h->read_off, b->view.read_off, 8 * ((size_t)n_reads + 1));

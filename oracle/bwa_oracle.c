@@ -1937,3 +1937,51 @@ int64_t orc_align_batch(const orc_index *idx, const orc_opts *o, const uint8_t *
     if (checksum) *checksum = ck;
     return err ? -1 : nreg;
 }
+
+/* ---- batch TSV (parity tests at config sizes) ----------------------------------------------- */
+typedef struct {
+    const orc_index *idx; const orc_opts *o; const uint8_t *const *reads; int lo, hi; uint64_t first_call;
+    char **rows; int err;
+} tsv_job_t;
+
+static void *tsv_worker(void *arg)
+{
+    tsv_job_t *j = arg;
+    for (int r = j->lo; r < j->hi; ++r) {
+        j->rows[r] = orc_align_tsv(j->idx, j->o, j->reads[r], orc_lrand48_at(j->first_call + (uint64_t)r));
+        if (!j->rows[r]) { j->err = 1; break; }
+    }
+    return NULL;
+}
+
+char *orc_align_tsv_batch(const orc_index *idx, const orc_opts *o, const uint8_t *const *reads, int n,
+                          uint64_t first_call, int threads, int64_t *rows_per_read)
+{
+    if (threads < 1) threads = 1;
+    char **rows = calloc((size_t)(n > 0 ? n : 1), sizeof(char *));
+    pthread_t *th = malloc(sizeof(pthread_t) * (size_t)threads);
+    tsv_job_t *jobs = calloc((size_t)threads, sizeof(tsv_job_t));
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (tsv_job_t){ idx, o, reads, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads),
+                               first_call, rows, 0 };
+        pthread_create(&th[t], NULL, tsv_worker, &jobs[t]);
+    }
+    int err = 0;
+    for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); err |= jobs[t].err; }
+    size_t total = 1;
+    for (int r = 0; r < n; ++r) total += rows[r] ? strlen(rows[r]) : 0;
+    char *out = err ? NULL : malloc(total), *p = out;
+    for (int r = 0; r < n; ++r) {
+        if (out) {
+            size_t l = strlen(rows[r]);
+            int64_t c = 0;
+            for (size_t i = 0; i < l; ++i) c += rows[r][i] == '\n';
+            if (rows_per_read) rows_per_read[r] = c;
+            memcpy(p, rows[r], l); p += l;
+        }
+        free(rows[r]);
+    }
+    if (out) *p = 0;
+    free(rows); free(th); free(jobs);
+    return out;
+}

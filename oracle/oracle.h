@@ -73,6 +73,12 @@ int64_t orc_lrand48_at(uint64_t pos);
  * ref_subseq is "*" on reverse-strand rows (Q7: the reference reads out of bounds there). */
 char *orc_align_tsv(const orc_index *idx, const orc_opts *opt, const uint8_t *nuclseq_read, int64_t lrand_id);
 
+/* orc_align_tsv over n reads (nuclseq pointers) on `threads` POSIX threads, read r with lrand48 call
+ * first_call + r; the rows concatenated in read order, rows_per_read[r] = rows of read r.  NULL if a read
+ * is unsupported.  malloc'd (orc_free). */
+char *orc_align_tsv_batch(const orc_index *idx, const orc_opts *opt, const uint8_t *const *reads, int n,
+                          uint64_t first_call, int threads, int64_t *rows_per_read);
+
 /* Raw alignment regions after mem_align1 (+ mem_reg2aln) for stage-level parity tests. */
 typedef struct {
     int64_t rb, re;

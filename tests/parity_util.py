@@ -48,3 +48,86 @@ def compare(pi, oi, read_texts, first_call=0, opts=None):
                 if getattr(a, f) != getattr(e, f):
                     bad.append((i, f, getattr(a, f), getattr(e, f)))
     return rows, bad
+
+
+def _oracle_batch_tsv(oi, oo, raws, first_call, threads=0):
+    """orc_align_tsv_batch: the oracle's rows of every read, read order, on all host cores."""
+    import ctypes
+    import os
+    n = len(raws)
+    bufs = [ctypes.create_string_buffer(r, len(r)) for r in raws]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in bufs])
+    cnt = (ctypes.c_int64 * max(n, 1))()
+    L = O.lib()
+    f = L.orc_align_tsv_batch
+    f.restype = ctypes.c_void_p
+    f.argtypes = [ctypes.c_void_p, ctypes.POINTER(O.OrcOpts), ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64,
+                  ctypes.c_int, ctypes.c_void_p]
+    p = f(oi.h, ctypes.byref(oo), ptrs, n, first_call, threads or min(16, os.cpu_count() or 1), cnt)
+    assert p, "oracle: unsupported read"
+    try:
+        text = ctypes.string_at(p).decode("latin-1")
+    finally:
+        L.orc_free(p)
+    return text, list(cnt)[:n]
+
+
+def gpu_batch_tsv(pi, seqs, opts, first_call):
+    """bsq_align_batch + bsq_render_tsv over the whole batch: (text, rows per read)."""
+    import ctypes
+    from bioseqdb_amd import _native as N
+    L = N.lib()
+    n = len(seqs)
+    pi.upload()
+    arr = (ctypes.c_void_p * max(n, 1))(*[s.ptr for s in seqs])
+    out = ctypes.POINTER(N.Hits)()
+    N.check(L.bsq_align_batch(pi.handle, ctypes.byref(opts), arr, n, first_call, ctypes.byref(out)))
+    try:
+        p = L.bsq_render_tsv(pi.handle, out, arr)
+        try:
+            text = ctypes.string_at(p).decode("latin-1")
+        finally:
+            L.bsq_free(p)
+        ro = out.contents.read_off
+        counts = [ro[i + 1] - ro[i] for i in range(n)]
+    finally:
+        L.bsq_hits_free(out)
+    return text, counts
+
+
+def compare_tsv(got_text, got_counts, exp_text, exp_counts, limit=50):
+    """Row-by-row comparison of two bwa_result TSVs in read order; the oracle prints '*' as ref_subseq on
+    reverse-strand rows (Q7), where that column is skipped.  Returns (rows, mismatches)."""
+    bad = []
+    g_lines = got_text.splitlines()
+    e_lines = exp_text.splitlines()
+    gi = ei = 0
+    rows = 0
+    for r, (gc, ec) in enumerate(zip(got_counts, exp_counts)):
+        if gc != ec:
+            bad.append((r, "n_rows", gc, ec))
+        else:
+            for k in range(gc):
+                a, e = g_lines[gi + k], e_lines[ei + k]
+                rows += 1
+                if a != e:
+                    fa, fe = a.split("\t"), e.split("\t")
+                    for j, (x, y) in enumerate(zip(fa, fe)):
+                        if x != y and not (j == 1 and y == "*"):
+                            bad.append((r, FIELDS[j], x[:60], y[:60]))
+        gi += gc
+        ei += ec
+        if len(bad) >= limit:
+            break
+    if len(got_counts) != len(exp_counts):
+        bad.append((-1, "n_reads", len(got_counts), len(exp_counts)))
+    return rows, bad
+
+
+def compare_batch(pi, oi, seqs, first_call=0, opts=None):
+    """The whole batch through the GPU (bsq_align_batch + bsq_render_tsv) against the oracle's batch TSV.
+    `seqs` are NucleotideSequence values; returns (rows, mismatches)."""
+    o = pi.options if opts is None else opts
+    got, gc = gpu_batch_tsv(pi, seqs, o, first_call)
+    exp, ec = _oracle_batch_tsv(oi, O.opts_from(o), [s.raw for s in seqs], first_call)
+    return compare_tsv(got, gc, exp, ec)
