@@ -87,6 +87,7 @@ SIGNATURES = {
                                        ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(Hits))]),
     "bsq_hits_free": (None, [ctypes.POINTER(Hits)]),
     "bsq_render_tsv": (_P, [_P, ctypes.POINTER(Hits), ctypes.POINTER(_P)]),
+    "bsq_index_ref_subseq": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "bsq_free": (None, [_P]),
     "bsq_batch_create": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(_P)]),
     "bsq_batch_free": (None, [_P]),

@@ -197,7 +197,11 @@ extern "C" int bsq_index_build(bsq_index *idx, int threads)
     return BSQ_OK;
 }
 
-extern "C" int64_t bsq_index_l_pac(const bsq_index *idx) { return idx ? idx->h.l_pac : -1; }
+// bns->l_pac = 4 * pac_forward.size() (bwa.cpp:118), known as soon as the rows are added
+extern "C" int64_t bsq_index_l_pac(const bsq_index *idx)
+{
+    return idx ? std::max<int64_t>(idx->h.l_pac, 4 * (int64_t)idx->h.pac.size()) : -1;
+}
 extern "C" int64_t bsq_index_seq_len(const bsq_index *idx) { return idx ? (int64_t)idx->h.seq_len : -1; }
 extern "C" int64_t bsq_index_primary(const bsq_index *idx) { return idx ? (int64_t)idx->h.primary : -1; }
 extern "C" int32_t bsq_index_n_refs(const bsq_index *idx) { return idx ? (int32_t)idx->h.anns.size() : -1; }

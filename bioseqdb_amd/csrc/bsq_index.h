@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -43,6 +45,25 @@ void ns_to_nt4(const uint8_t *ns, std::vector<uint8_t> &out);
 
 struct DeviceIndex;   // bsq_api.cpp
 
+struct HoleRef { int64_t beg, end; uint32_t order; char amb; };
+
+// Holes ordered by offset, with the longest length: the holes overlapping [rb, re) are those with offset
+// in (rb - max_len, re).  Overlapping holes (Q3: offsets of different rows share one axis) are applied
+// in their original order, as extract_reference_subseq's loop does (bioseqdb/bwa.cpp:61-66).
+struct HoleIndex {
+    std::vector<HoleRef> by_off;
+    int64_t max_len = 0;
+    explicit HoleIndex(const std::vector<Hole> &holes)
+    {
+        by_off.reserve(holes.size());
+        for (size_t i = 0; i < holes.size(); ++i) {
+            by_off.push_back(HoleRef{holes[i].offset, holes[i].offset + holes[i].len, (uint32_t)i, holes[i].amb});
+            max_len = std::max<int64_t>(max_len, holes[i].len);
+        }
+        std::sort(by_off.begin(), by_off.end(), [](const HoleRef &a, const HoleRef &b) { return a.beg < b.beg; });
+    }
+};
+
 struct HostIndex {
     std::vector<uint8_t> pac;    // pac_forward
     std::vector<Hole> holes;     // unshifted offsets (Q3)
@@ -77,4 +98,8 @@ struct bsq_index {
     bsq::HostIndex h;
     std::mutex pool_mu;
     bsq_batch *pool = nullptr;
+    // offset-ordered holes for host rendering, built on first use after the index is built
+    std::once_flag hx_once;
+    std::unique_ptr<bsq::HoleIndex> hx;
+    const bsq::HoleIndex &holes() { std::call_once(hx_once, [this] { hx.reset(new bsq::HoleIndex(h.holes)); }); return *hx; }
 };

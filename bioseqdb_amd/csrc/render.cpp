@@ -20,25 +20,6 @@ using namespace bsq;
 
 namespace {
 
-struct HoleRef { int64_t beg, end; uint32_t order; char amb; };
-
-// Holes ordered by offset, with the longest length: the holes overlapping [rb, re) are those with
-// offset in (rb - max_len, re).  Overlapping holes (Q3: offsets of different rows share one axis) are
-// applied in their original order, as the reference's loop does.
-struct HoleIndex {
-    std::vector<HoleRef> by_off;
-    int64_t max_len = 0;
-    explicit HoleIndex(const std::vector<Hole> &holes)
-    {
-        by_off.reserve(holes.size());
-        for (size_t i = 0; i < holes.size(); ++i) {
-            by_off.push_back(HoleRef{holes[i].offset, holes[i].offset + holes[i].len, (uint32_t)i, holes[i].amb});
-            max_len = std::max<int64_t>(max_len, holes[i].len);
-        }
-        std::sort(by_off.begin(), by_off.end(), [](const HoleRef &a, const HoleRef &b) { return a.beg < b.beg; });
-    }
-};
-
 void ref_subseq(const HostIndex &h, const HoleIndex &hx, int64_t rb, int64_t re, std::string &out)
 {
     const size_t base = out.size();
@@ -128,10 +109,20 @@ int render_threads(int64_t n_hits)
 
 }  // namespace
 
+extern "C" int64_t bsq_index_ref_subseq(const bsq_index *idx, int64_t rb, int64_t re, char *out)
+{
+    if (!idx || !idx->h.built || rb < 0 || re < rb || re > 2 * idx->h.l_pac) return -1;
+    if (!out) return re - rb;
+    std::string s;
+    ref_subseq(idx->h, const_cast<bsq_index *>(idx)->holes(), rb, re, s);
+    memcpy(out, s.data(), s.size());
+    return (int64_t)s.size();
+}
+
 extern "C" char *bsq_render_tsv(const bsq_index *idx, const bsq_hits *hits, const void *const *reads)
 {
     if (!idx || !hits) return nullptr;
-    const HoleIndex hx(idx->h.holes);
+    const HoleIndex &hx = const_cast<bsq_index *>(idx)->holes();
     const int32_t n = hits->n_reads;
     const int T = n > 0 ? render_threads(hits->n_hits) : 1;
     std::vector<std::string> part((size_t)T);

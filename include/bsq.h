@@ -174,6 +174,10 @@ void bsq_hits_free(bsq_hits *hits);
  * ref_subseq on reverse-strand rows, where the reference reads out of bounds (Q7), is rendered
  * as the reverse-strand reference text.  Returns a malloc'd string (free with bsq_free). */
 char *bsq_render_tsv(const bsq_index *idx, const bsq_hits *hits, const void *const *reads);
+/* ref_subseq of one row (extract_reference_subseq, bioseqdb/bwa.cpp:55-68, Q3 hole overlay; reverse-strand
+ * text where the reference reads out of bounds, Q7): writes re - rb characters (no NUL) to out and returns
+ * that count; out == NULL: returns the count only.  -1 for an unbuilt index or a range outside [0, 2*l_pac). */
+int64_t bsq_index_ref_subseq(const bsq_index *idx, int64_t rb, int64_t re, char *out);
 void bsq_free(void *p);
 
 /* ---- device-resident batches (bench / multi-GPU drivers) --------------------------------------- */

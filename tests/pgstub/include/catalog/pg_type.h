@@ -1,0 +1,2 @@
+/* test stub (see postgres.h): everything lives in postgres.h */
+#include "postgres.h"
