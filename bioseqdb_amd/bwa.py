@@ -3,7 +3,7 @@
 Reference interface being mirrored (same names, argument meaning and error behaviour):
   * ``NucleotideSequence`` / ``nuclseq_in``            bioseqdb/sequence.h:18-38, extension.cpp:46-61
   * ``bwa_opts()`` incl. the ROW field-order quirk Q1  bioseqdb/bioseqdb--0.0.0.sql:160-194
-  * ``BwaIndex`` (add_ref_sequence/build/align_sequence) bioseqdb/bwa.h:32-48, bwa.cpp:129-230
+  * ``BwaIndex`` (add_ref_sequence/build/align_sequence) bioseqdb/bwa.h:32-48, bwa.cpp:80-181
   * ``BwaMatch`` / ``bwa_result`` rows                  bwa.h:15-30, bioseqdb--0.0.0.sql:196-212
   * ``nuclseq_search_bwa`` / ``nuclseq_multi_search_bwa`` extension.cpp:311-378
 The SQL strings of the reference become Python iterables of ``(id, nuclseq)`` rows (the SPI cursor
@@ -260,7 +260,7 @@ class BwaIndex:
                         first_call: Optional[int] = None) -> List[List[BwaMatch]]:
         """BwaIndex::align_sequence for a cursor batch; consumes one lrand48 value per read."""
         n = len(seqs)
-        if self.l_pac <= 0:   # bwa.cpp:191: empty reference -> no matches, no mem_align1 call
+        if self.l_pac <= 0:   # bwa.cpp:142-143: empty reference -> no matches, no mem_align1 call
             return [[] for _ in range(n)]
         self.upload()
         if first_call is None:

@@ -1,5 +1,5 @@
 // align_kernels.hip -- HIP (gfx950) kernels of the BWA-MEM alignment path behind bioseqdb's
-// nuclseq_search_bwa / nuclseq_multi_search_bwa (reference: bioseqdb/bwa.cpp:190-230, which calls
+// nuclseq_search_bwa / nuclseq_multi_search_bwa (reference: bioseqdb/bwa.cpp:141-181, which calls
 // libbwa mem_align1 + mem_reg2aln).  The libbwa algorithm is re-expressed as five stage kernels over
 // device-resident index data; results must equal libbwa's bit for bit (checked against oracle/).
 //
@@ -11,6 +11,7 @@
 //
 // Round-1 mapping: one read per lane (inter-task parallelism) with private scratch in HBM;
 // reads that overflow the small per-read slots are re-run by the host with large capacities.
+// Restates algorithms of BWA (lh3/bwa, Apache-2.0) and klib (MIT) for bit-exact results; see NOTICE.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <algorithm>
@@ -678,7 +679,6 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
 {
     int i, j, oe_del = o_del + e_del, oe_ins = o_ins + e_ins, beg, end, max, max_i, max_j, max_ins, max_del, max_ie,
         gscore, max_off;
-    if (o.exp_flags & 1) { *_qle = *_tle = *_gtle = 0; *_gscore = -1; *_max_off = 0; return h0; }
     const Score sc = score_of(o);
     if (qlen < 0) qlen = 0;
     // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
@@ -1115,13 +1115,6 @@ DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int 
                  EhSmall ehx, uint64_t &cells)
 {
     // inlined: an out-of-line call spills the caller's live VGPRs to scratch around every extension
-    if (o.exp_flags & 8) {   // timing experiment: DP cycles land in the cell counter
-        const uint64_t t0 = clock64();
-        const int r = ksw_extend2_body(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0,
-                                       qle, tle, gtle, gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
-        cells += clock64() - t0;
-        return r;
-    }
     return ksw_extend2_body(o, qlen, query, tlen, target, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop, h0, qle, tle,
                             gtle, gscore, max_off, EhRing{ehx.ovf, ehx.lane}, cells);
 }
@@ -1397,7 +1390,6 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
     X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
     X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
-    const uint64_t t_k0 = clock64();
     for (int it = tid; it < n; it += nthr) {
         const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;
@@ -1425,15 +1417,12 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
                 chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
         }
         if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
-        const uint64_t t1 = clock64();
         X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
         mark_primary_se(o, X, ids[r]);
         n_regs[li] = X.n;
-        if (o.exp_flags & 8) bases += clock64() - t1;   // timing experiment: dedup + primary cycles
     }
     wave_add(&ctr[STG_EXTEND].dp_cells, cells);
     wave_add(&ctr[STG_EXTEND].ref_bases, bases);
-    if (o.exp_flags & 8) wave_add(&ctr[STG_EXTEND].sa_values, clock64() - t_k0);   // timing experiment
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1692,8 +1681,7 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 &&
                      (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
-        static const size_t sh_env = getenv("BSQ_EXT_SH") ? (size_t)atol(getenv("BSQ_EXT_SH")) : 0;   // tuning only
-        const size_t sh = std::max((size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2), sh_env);
+        const size_t sh = (size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2);
         hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
                            seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
     } else {

@@ -2,7 +2,7 @@
 // management, kernel orchestration on a per-batch HIP stream, overflow retry, result packing.
 //
 // Host-side orchestration of the path that bioseqdb runs as BwaIndex::align_sequence per cursor row
-// (bioseqdb/bwa.cpp:190-230, bioseqdb/extension.cpp:362-370).  There is no CPU fallback: every
+// (bioseqdb/bwa.cpp:141-181, bioseqdb/extension.cpp:362-370).  There is no CPU fallback: every
 // alignment result comes from the HIP kernels in align_kernels.hip; without a device the calls fail
 // with BSQ_E_NODEV.
 #include <hip/hip_runtime.h>
@@ -55,8 +55,6 @@ hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int);
-hipError_t launch_smem_flat(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
-                            int, Intv *, int32_t *, uint32_t *, Counters *, int, int);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
 struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
 struct RenderView {
@@ -742,7 +740,6 @@ DOpts make_dopts(const bsq_opts &o)
     d.max_mem_intv = 20; d.split_factor = 1.5f; d.mask_level = 0.50f; d.drop_ratio = 0.50f; d.mask_level_redun = 0.95f;
     // mem_opt_init fills mat with a=1, b=4 and bioseqdb never refills it (Q2)
     d.mat_match = 1; d.mat_mismatch = -4; d.mat_amb = -1; d.mat_max = 1;
-    { const char *e = getenv("BSQ_EXP"); d.exp_flags = e ? atoi(e) : 0; }   // timing experiments only
     return d;
 }
 
@@ -1021,17 +1018,12 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     hipStream_t st = b->stream;
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
-        const int lcap_env = getenv("BSQ_LCAP") ? atoi(getenv("BSQ_LCAP")) : 0;   // tuning and the spill test
-        // 15 entries in LDS = 38.4 KB per 256-lane block: 4 blocks (16 waves) per CU; longer lists spill
+        // 15 entries in LDS = 38.4 KB per 256-lane block: 4 blocks (16 waves) per CU; longer lists spill.
+        // BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested (tests/test_gpu_parity.py).
+        const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
         const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 8;
-        static const char *alt = getenv("BSQ_SMEM");
-        static const int sblocks = getenv("BSQ_SMEM_BLOCKS") ? atoi(getenv("BSQ_SMEM_BLOCKS")) : 0;
-        if (alt && !strcmp(alt, "flat"))   // experimental persistent-lane variant (smem.hip)
-            HIPCHK(launch_smem_flat(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
-                                    sblocks));
-        else
-            HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
-                                   w.lspill, tiny_caps() ? 0 : LSPILL));
+        HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
+                               w.lspill, tiny_caps() ? 0 : LSPILL));
     } else {
         HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }
@@ -1053,8 +1045,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
                                 w.n_chains, w.status, w.sscore, w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
     const int32_t *order = nullptr;
-    static const bool no_sort = getenv("BSQ_EXT_SORT") && getenv("BSQ_EXT_SORT")[0] == '0';
-    if (!sel && w.ekey0 && n > 0 && !no_sort) {
+    if (!sel && w.ekey0 && n > 0) {
         // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
         HIPCHK(launch_ext_key(st, w.cp, (b->offs + b->lo), sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
         size_t tb = w.esort_bytes;
@@ -1071,8 +1062,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes - q_bytes) & ~15;
         // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
         const int32_t *r_order = nullptr;
-        static const bool no_rsort = getenv("BSQ_R2A_SORT") && getenv("BSQ_R2A_SORT")[0] == '0';
-        if (w.ekey0 && !no_rsort) {
+        if (w.ekey0) {
             // group balance: reads in order of their band class (the extension's sort buffers are free now)
             HIPCHK(launch_r2a_key(st, o, w.cp, (b->offs + b->lo), n, w.regs, w.n_regs, w.status, w.ekey0, w.eidx0, w.dcount + 2));
             size_t tb = w.esort_bytes;
@@ -1353,7 +1343,6 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
-        if (o.exp_flags & 8) b->stage_work[STG_CHAIN] = (double)c[STG_EXTEND].sa_values;   // timing experiment
     } else {
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
@@ -1512,7 +1501,6 @@ extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
         b->stage_bytes[STG_SMEM] =
             32.0 * c[STG_SMEM].occ_blocks + 16.0 * c[STG_SMEM].kmer_hits + (double)b->h_offs[n] / 4.0 * 1.0;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
-        if (o.exp_flags & 8) b->stage_work[STG_CHAIN] = (double)c[STG_EXTEND].sa_values;   // timing experiment
     }
     b->seeded = true;
     return BSQ_OK;
@@ -1717,7 +1705,7 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     if (!h) { set_err("out of memory"); return BSQ_E_NOMEM; }
     h->n_reads = n_reads;
     if (!idx->h.built) { free(h); set_err("index not built"); return BSQ_E_INVALID; }
-    if (idx->h.seq_len == 0 || n_reads == 0) {   // empty reference: align_sequence returns {} (bwa.cpp:191)
+    if (idx->h.seq_len == 0 || n_reads == 0) {   // empty reference: align_sequence returns {} (bwa.cpp:142-143)
         h->read_off = (int64_t *)calloc((size_t)n_reads + 1, 8);
         *out = h;
         return BSQ_OK;

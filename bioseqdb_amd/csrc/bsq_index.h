@@ -1,5 +1,5 @@
 // bsq_index.h -- host-side index object behind the C-ABI (replaces bioseqdb's BwaIndex storage,
-// bioseqdb/bwa.h:32-48, and libbwa's bwt_t/bntseq_t built in BwaIndex::build, bwa.cpp:156-177).
+// bioseqdb/bwa.h:32-48, and libbwa's bwt_t/bntseq_t built in BwaIndex::build, bwa.cpp:107-128).
 #pragma once
 #include <stdint.h>
 
@@ -39,7 +39,7 @@ inline int nt4(unsigned char c)
     default: return 4;
     }
 }
-// to_text rendering (sequence.cpp:71-81) and nt4 coding of a read (bwa.cpp:195 + mem_align1_core)
+// to_text rendering (sequence.cpp:71-81) and nt4 coding of a read (bwa.cpp:146 + mem_align1_core)
 std::string ns_to_text(const uint8_t *ns);
 void ns_to_nt4(const uint8_t *ns, std::vector<uint8_t> &out);
 

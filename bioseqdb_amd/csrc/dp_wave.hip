@@ -10,6 +10,7 @@
 //   * the traceback matrix z (one byte per cell, same bits as ksw) is written row by row into LDS,
 //     coalesced, and walked back uniformly.
 // Integer arithmetic only; results equal the serial ksw_global2 cell for cell.
+// Restates algorithms of BWA (lh3/bwa, Apache-2.0) and klib (MIT) for bit-exact results; see NOTICE.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,7 +74,7 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QA query, int tlen, TAcc target,
     lds_fence();
     TStream ts;
     if (tlen > 0) ts.init(*target.ix, target.start, target.dir);
-    for (int i = 0; i < ((o.exp_flags & 4) ? 0 : tlen); ++i) {
+    for (int i = 0; i < tlen; ++i) {
         const int tb = ts.next();   // uniform; next pac word prefetched
         const int beg = i > w ? i - w : 0;
         const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
@@ -117,7 +118,6 @@ DEV int ksw_global2_w(const DOpts &o, int qlen, QA query, int tlen, TAcc target,
         lds_fence();
     }
     const int score = eh[qlen].x;
-    if (z && (o.exp_flags & 2)) { cig[0] = (uint32_t)qlen << 4; *ncig = 1; return score; }
     if (z) {
         int n = 0, which = 0, i = tlen - 1;
         int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
@@ -310,7 +310,7 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
         const int min_w = dl + 3;
         w = w > min_w ? w : min_w;
         const int n_col = l_query < 2 * w + 1 ? l_query : 2 * w + 1;
-        if (n_col <= 64 && rlen < (int64_t)l_query + w && rlen <= 1024 && l_query <= 512 && !(o.exp_flags & 4)) {
+        if (n_col <= 64 && rlen < (int64_t)l_query + w && rlen <= 1024 && l_query <= 512) {
             // register-resident rows and sequences; traceback matrix in LDS (z_off >= 0) or the global slab
             if ((int64_t)n_col * rlen > zcap) { ovf = true; return 0; }
             const bool zl = z_off >= 0;
@@ -319,7 +319,6 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
                                                 nullptr, cells)
                         : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
                                                  (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
-            if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
             if (zl) traceback_w<true, 64>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
             else traceback_w<false, 64>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
         } else {
@@ -591,7 +590,7 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
     const int min_w = dl + 3;
     w = w > min_w ? w : min_w;
     const int n_col = l_query < 2 * w + 1 ? l_query : 2 * w + 1;
-    if (n_col > G || rlen >= (int64_t)l_query + w || rlen > tcap || (int64_t)n_col * rlen > zcap || (o.exp_flags & 4)) {
+    if (n_col > G || rlen >= (int64_t)l_query + w || rlen > tcap || (int64_t)n_col * rlen > zcap) {
         dfr = true;
         return 0;
     }
@@ -600,7 +599,6 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
     lds_fence();
     *score = ksw_global2_g<G>(sc, l_query, q_off, q_start, q_dir, t_off, (int)rlen, o.o_del, o.e_del, o.o_ins,
                               o.e_ins, w, n_col, z_off, cells, gl);
-    if (o.exp_flags & 2) { cig[0] = (uint32_t)l_query << 4; *ncig = 1; return 1; }
     traceback_w<true, G>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf, gl, lane_id() & ~(G - 1));
     return 1;
 }

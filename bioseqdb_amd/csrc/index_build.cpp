@@ -1,6 +1,6 @@
 // index_build.cpp -- host construction of the alignment index (the step before the hot path).
 //
-// Replaces BwaIndex::add_ref_sequence / BwaIndex::build (bioseqdb/bwa.cpp:131-177): the reference
+// Replaces BwaIndex::add_ref_sequence / BwaIndex::build (bioseqdb/bwa.cpp:82-128): the reference
 // rows are concatenated byte-aligned exactly as the reference does (Q3/Q4), the text
 // T = pac || revcomp(pac) is suffix-sorted (the BWT of T$ is unique, so any correct suffix sort
 // reproduces libbwa's is_bwt + bwt_cal_sa output), and the result is laid out for HBM:

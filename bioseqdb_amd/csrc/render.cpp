@@ -1,5 +1,5 @@
 // render.cpp -- bwa_result row rendering (reference: BwaIndex::align_sequence's BwaMatch fields,
-// bioseqdb/bwa.cpp:198-226, extract_reference_subseq :104-117, cigar_compressed_to_string :119-126,
+// bioseqdb/bwa.cpp:159-175, extract_reference_subseq :55-68, cigar_compressed_to_string :70-77,
 // and the htslib bam_cigar_opchr table "MIDNSHP=XB", so libbwa's clip op 3 prints as 'N' -- Q8).
 //
 // Host materialisation: once alignment runs on the GPU, rendering the rows is the

@@ -1,7 +1,7 @@
 // render_gpu.hip -- bwa_result rows rendered on the GPU (host materialisation).
 //
 // The same bytes as bsq_render_tsv (render.cpp; reference: BwaIndex::align_sequence's BwaMatch fields,
-// bioseqdb/bwa.cpp:198-226, extract_reference_subseq :104-117, cigar_compressed_to_string :119-126):
+// bioseqdb/bwa.cpp:159-175, extract_reference_subseq :55-68, cigar_compressed_to_string :70-77):
 // one thread per row, in two passes -- the exact length of every row, an exclusive scan for the row
 // offsets, then the text itself -- so the host receives one finished buffer.  ref_subseq comes from
 // the pac in HBM with the reference's hole overlay (Q3: row-relative offsets on the concatenated axis,

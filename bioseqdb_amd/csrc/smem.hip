@@ -11,6 +11,7 @@
 //  * smem1's per-call output (mem1) is staged at the tail of the read's output slot.
 // Reads that exceed the LDS list or the output slot are flagged and re-run by the large-capacity
 // kernel k_smem (align_kernels.hip).  Output is identical to k_smem, interval for interval.
+// Restates algorithms of BWA (lh3/bwa, Apache-2.0) and klib (MIT) for bit-exact results; see NOTICE.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -473,307 +474,6 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
         size_t sh = lds_bytes<uint64_t>(T, lcap);
         hipLaunchKernelGGL(k_smem_lds<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
                            status, ctr, lcap, spill, gcap);
-    }
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_smem_flat: the same computation as k_smem_lds restated as a per-lane state machine whose loop
-// issues exactly one bwt_extend per lane per iteration, whichever part of mem_collect_intv the lane
-// is in (smem1 forward / backward, pass 2, seed strategy), and persistent lanes: a lane that
-// finishes its read takes the next one (grid-stride), so lanes never idle behind the slowest read
-// of their wave.  Two restatements make this possible without changing the output:
-//  * the forward list is walked top-down in place instead of being reversed (logical entry j of
-//    the backward phase is physical entry top - j; the compacted list is written at top - nc,
-//    never above an entry still to be read);
-//  * mem1 is filtered straight into the output slot at emission: mem_collect_intv only appends the
-//    entries with end - start >= min_seed_len and the slot is sorted by info at the end, where equal
-//    keys are identical intervals, so the append order cannot show.
-enum : int { PH_NEXT = 0, PH_SEEK1, PH_FWD, PH_BWD, PH_SEEK2, PH_SEEKS, PH_STF, PH_FIN, PH_EXIT };
-
-template <typename X>
-__global__ void __launch_bounds__(256) k_smem_flat(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
-                                                   const int64_t *offs, int n, Intv *intv_out, int32_t *n_intv,
-                                                   uint32_t *status, Counters *ctr, int lcap)
-{
-    extern __shared__ uint8_t lds_raw[];
-    const int T = blockDim.x, t = threadIdx.x;
-    X *Lx0 = reinterpret_cast<X *>(lds_raw) + t;
-    X *Lx2 = reinterpret_cast<X *>(lds_raw) + (size_t)T * lcap + t;
-    uint16_t *Lend = reinterpret_cast<uint16_t *>(lds_raw + (size_t)2 * T * lcap * sizeof(X)) + t;
-    FM<X> fm;
-    fm.occ = ix.occ;
-    fm.occ32 = ix.occ32;
-    fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
-    fm.primary = (X)ix.primary;
-    fm.kt = nullptr;
-    fm.K = 0;
-    const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
-    const int min_seed_len = o.min_seed_len;
-    const uint64_t split_width = (uint64_t)o.split_width;
-    const int max_mem_intv = o.max_mem_intv;
-    const int stride = gridDim.x * T;
-    uint64_t nblk = 0;
-
-    int li = blockIdx.x * T + t - stride;
-    const uint8_t *q = codes;
-    int len = 0, sn = 0, cap = cp.intv;
-    Intv *out = intv_out;
-    bool ovf = false;
-    int phase = PH_NEXT, pass = 1;
-    int x = 0, k = 0, old_n = 0;
-    int sx = 0, i = 0, ikend = 0, nl = 0, ret = 0, n1 = 0, last_start = 0, bi = 0, j = 0, nc = 0, cb = 0, top = 0;
-    int ee = 0;
-    X minI = 1, ik0 = 0, ik1 = 0, ik2 = 0, last_x2 = 0, e0 = 0, e2 = 0;
-    X ea = 0, eo = 0, ex2 = 0;
-    int ec = 0;
-    X r_new = 0, r_oth = 0, r_2 = 0;
-    bool have_res = false;
-    // one-ahead prefetch of the base the lane will need next (issued with the extend's loads)
-    int qp_pos = -1, qp_val = 0, pp = -1;
-    auto getq = [&](int pos) -> int { return pos == qp_pos ? qp_val : (int)q[pos]; };
-
-    bool want = false;
-    for (;;) {
-        // slow path: lanes without a pending request run the full machine until they have one
-        while (!want && phase != PH_EXIT) {
-            if (phase == PH_FWD || phase == PH_STF) {
-                if (have_res) {
-                    have_res = false;
-                    if (phase == PH_FWD) {
-                        if (r_2 != ik2) {
-                            if (nl >= lcap) { ovf = true; phase = PH_FIN; continue; }
-                            Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl;
-                            if (r_2 < minI) goto start_bwd;
-                        }
-                        ikend = i + 1;
-                    } else if (r_2 < (X)max_mem_intv && i - sx >= min_seed_len) {
-                        if (r_2 > 0) {
-                            if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
-                            Intv m;
-                            m.x[0] = r_oth; m.x[1] = r_new; m.x[2] = r_2;
-                            m.info = (uint64_t)sx << 32 | (uint64_t)(i + 1);
-                            out[sn++] = m;
-                        }
-                        x = i + 1; phase = PH_SEEKS; continue;
-                    }
-                    ik0 = r_oth; ik1 = r_new; ik2 = r_2; ++i;
-                }
-                {
-                    const int cur = i < len ? getq(i) : 4;
-                    if (cur < 4) {
-                        ea = ik1; eo = ik0; ex2 = ik2; ec = 3 - cur; want = true;
-                        pp = i + 1 < len ? i + 1 : -1;
-                        continue;
-                    }
-                }
-                if (phase == PH_STF) { x = i < len ? i + 1 : len; phase = PH_SEEKS; continue; }
-                // ambiguous base or end of read: push the current interval and turn backwards
-                if (nl >= lcap) { ovf = true; phase = PH_FIN; continue; }
-                Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl;
-            start_bwd:
-                top = nl - 1;
-                ret = Lend[top * T];
-                last_start = 0x7fffffff;
-                bi = sx - 1;
-                cb = bi < 0 ? -1 : (q[bi] < 4 ? q[bi] : -1);
-                j = 0; nc = 0; last_x2 = 0;
-                phase = PH_BWD;
-                continue;
-            }
-            if (phase == PH_BWD) {
-                bool hit = false;
-                if (have_res) {
-                    have_res = false;
-                    if (r_2 < minI) hit = true;
-                    else {
-                        if (nc == 0 || r_2 != last_x2) {
-                            const int p = (top - nc) * T;
-                            Lx0[p] = r_new; Lx2[p] = r_2; Lend[p] = (uint16_t)ee;
-                            ++nc; last_x2 = r_2;
-                        }
-                        ++j;
-                    }
-                } else if (j < nl) {
-                    const int p = (top - j) * T;
-                    e0 = Lx0[p]; e2 = Lx2[p]; ee = Lend[p];
-                    if (cb >= 0) { ea = e0; eo = 0; ex2 = e2; ec = cb; want = true; pp = bi - 1; continue; }
-                    hit = true;
-                } else {
-                    if (nc == 0) {   // smem1 returns
-                        if (pass == 1) { x = ret; phase = PH_SEEK1; }
-                        else { ++k; phase = PH_SEEK2; }
-                        continue;
-                    }
-                    nl = nc; --bi;
-                    cb = bi < 0 ? -1 : getq(bi);
-                    cb = cb < 4 ? cb : -1;
-                    j = 0; nc = 0; last_x2 = 0;
-                    continue;
-                }
-                if (hit) {
-                    if (nc == 0 && (n1 == 0 || bi + 1 < last_start)) {
-                        ++n1; last_start = bi + 1;
-                        if (ee - (bi + 1) >= min_seed_len) {
-                            if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
-                            Intv m;
-                            m.x[0] = e0; m.x[1] = 0; m.x[2] = e2;
-                            m.info = (uint64_t)(uint32_t)(bi + 1) << 32 | (uint32_t)ee;
-                            out[sn++] = m;
-                        }
-                    }
-                    ++j;
-                }
-                continue;
-            }
-            if (phase == PH_SEEK1 || phase == PH_SEEK2) {
-                int at = -1, mi = 1;
-                if (phase == PH_SEEK1) {
-                    if (x < len) {
-                        if (q[x] < 4) at = x;
-                        else { ++x; continue; }
-                    } else { old_n = sn; k = 0; phase = PH_SEEK2; continue; }
-                    pass = 1;
-                } else {
-                    if (k < old_n) {
-                        const Intv p = out[k];
-                        const int st = (int)(p.info >> 32), en = (int)(uint32_t)p.info;
-                        if (en - st < split_len || p.x[2] > split_width) { ++k; continue; }
-                        at = (st + en) >> 1; mi = (int)p.x[2] + 1;
-                    } else { x = 0; phase = max_mem_intv > 0 ? PH_SEEKS : PH_FIN; continue; }
-                    pass = 2;
-                }
-                // bwt_smem1a entry
-                sx = at; n1 = 0; minI = (X)(mi < 1 ? 1 : mi);
-                const int c0 = q[at];
-                if (c0 > 3) {
-                    if (pass == 1) { x = at + 1; } else { ++k; }
-                    continue;
-                }
-                ik0 = fm.L2(c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0); ik1 = fm.L2(3 - c0) + 1;
-                ikend = at + 1; nl = 0; i = at + 1;
-                phase = PH_FWD;
-                continue;
-            }
-            if (phase == PH_SEEKS) {
-                if (x < len) {
-                    const int c0 = q[x];
-                    if (c0 > 3) { ++x; continue; }
-                    sx = x; i = x + 1;
-                    ik0 = fm.L2(c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0); ik1 = fm.L2(3 - c0) + 1;
-                    phase = PH_STF;
-                } else phase = PH_FIN;
-                continue;
-            }
-            if (phase == PH_FIN) {
-                if (ovf) {
-                    status[li] |= ST_OVERFLOW;
-                    n_intv[li] = 0;
-                } else {
-                    for (int a = 1; a < sn; ++a) {   // equal keys are identical intervals: any correct sort is exact
-                        const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
-                        int b = a;
-                        for (; b > 0; --b) {
-                            const uint64_t pi = out[b - 1].info;
-                            if (!(ti < pi)) break;
-                            out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
-                            out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
-                        }
-                        out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
-                    }
-                    n_intv[li] = sn;
-                }
-                phase = PH_NEXT;
-                continue;
-            }
-            // PH_NEXT
-            li += stride;
-            if (li >= n) { phase = PH_EXIT; continue; }
-            q = codes + offs[li];
-            len = (int)(offs[li + 1] - offs[li]);
-            out = intv_out + (size_t)li * cp.intv;
-            sn = 0; ovf = false; x = 0; qp_pos = -1;
-            phase = PH_SEEK1;
-        }
-        if (!__any(want)) break;
-        if (!want) continue;
-        if (pp >= 0 && pp != qp_pos) { qp_val = q[pp]; qp_pos = pp; }
-        extend1(fm, ea, eo, ex2, ec, r_new, r_oth, r_2, nblk);
-        // fast path: consume the result and issue the next request for the common steps; anything
-        // else leaves the result to the machine above (same state updates either way)
-        want = false;
-        if (phase == PH_FWD || phase == PH_STF) {
-            const int nxt = i + 1;
-            const int cur = nxt < len ? getq(nxt) : 4;
-            const bool fwd = phase == PH_FWD;
-            const bool changed = r_2 != ik2;
-            const bool stop = fwd ? (changed && r_2 < minI) : (r_2 < (X)max_mem_intv && i - sx >= min_seed_len);
-            if (!stop && cur < 4 && !(fwd && changed && nl >= lcap)) {
-                if (fwd && changed) { Lx0[nl * T] = ik0; Lx2[nl * T] = ik2; Lend[nl * T] = (uint16_t)ikend; ++nl; }
-                ikend = nxt; ik0 = r_oth; ik1 = r_new; ik2 = r_2; i = nxt;
-                ea = ik1; eo = ik0; ex2 = ik2; ec = 3 - cur; want = true;
-                pp = nxt + 1 < len ? nxt + 1 : -1;
-            } else have_res = true;
-        } else {   // PH_BWD: apply, then the next entry (or the next position when the level is done)
-            if (r_2 < minI) {
-                if (nc == 0 && (n1 == 0 || bi + 1 < last_start)) {
-                    ++n1; last_start = bi + 1;
-                    if (ee - (bi + 1) >= min_seed_len) {
-                        if (sn >= cap) { ovf = true; phase = PH_FIN; continue; }
-                        Intv m;
-                        m.x[0] = e0; m.x[1] = 0; m.x[2] = e2;
-                        m.info = (uint64_t)(uint32_t)(bi + 1) << 32 | (uint32_t)ee;
-                        out[sn++] = m;
-                    }
-                }
-            } else if (nc == 0 || r_2 != last_x2) {
-                const int p = (top - nc) * T;
-                Lx0[p] = r_new; Lx2[p] = r_2; Lend[p] = (uint16_t)ee;
-                ++nc; last_x2 = r_2;
-            }
-            ++j;
-            if (j == nl && nc > 0) {
-                nl = nc; --bi;
-                cb = bi < 0 ? -1 : getq(bi);
-                cb = cb < 4 ? cb : -1;
-                j = 0; nc = 0; last_x2 = 0;
-            }
-            if (j < nl && cb >= 0) {
-                const int p = (top - j) * T;
-                e0 = Lx0[p]; e2 = Lx2[p]; ee = Lend[p];
-                ea = e0; eo = 0; ex2 = e2; ec = cb; want = true; pp = bi - 1;
-            }
-        }
-    }
-    wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
-}
-
-hipError_t launch_smem_flat(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
-                            const int64_t *offs, int n, Intv *intv, int32_t *n_intv, uint32_t *status, Counters *ctr,
-                            int lcap, int max_blocks)
-{
-    const int T = 256;
-    int grid = (n + T - 1) / T;
-    if (grid == 0) return hipSuccess;
-    auto clamp = [&](const void *fn, size_t sh) {
-        // persistent lanes: one resident wave of blocks (or max_blocks when given)
-        int dev = 0, cus = 0, per = 0;
-        if (max_blocks <= 0 && hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, T, sh) == hipSuccess && per > 0)
-            max_blocks = cus * per;
-        if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
-    };
-    if (!ix.wide) {
-        size_t sh = lds_bytes<uint32_t>(T, lcap);
-        clamp(reinterpret_cast<const void *>(k_smem_flat<uint32_t>), sh);
-        hipLaunchKernelGGL(k_smem_flat<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap);
-    } else {
-        size_t sh = lds_bytes<uint64_t>(T, lcap);
-        clamp(reinterpret_cast<const void *>(k_smem_flat<uint64_t>), sh);
-        hipLaunchKernelGGL(k_smem_flat<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap);
     }
     return hipGetLastError();
 }

@@ -6,12 +6,12 @@
  * longjmp cross it).  Each one replaces a piece of the reference's in-process seam
  * (bioseqdb/bwa.h:32-48 `class BwaIndex` over libbwa):
  *
- *   bsq_index_create / bsq_index_free  <- BwaIndex::BwaIndex / ~BwaIndex        (bwa.cpp:129, 180-188)
- *   bsq_index_add_ref                  <- BwaIndex::add_ref_sequence            (bwa.cpp:131-154)
- *   bsq_index_build                    <- BwaIndex::build                       (bwa.cpp:156-177)
+ *   bsq_index_create / bsq_index_free  <- BwaIndex::BwaIndex / ~BwaIndex        (bwa.cpp:80, 131-139)
+ *   bsq_index_add_ref                  <- BwaIndex::add_ref_sequence            (bwa.cpp:82-105)
+ *   bsq_index_build                    <- BwaIndex::build                       (bwa.cpp:107-128)
  *                                         = pac2bwt + is_bwt + bwt_bwtupdate_core + bwt_cal_sa
  *   bsq_index_upload                   <- (new) copies BWT/occ, SA and pac into HBM once
- *   bsq_align_batch                    <- BwaIndex::align_sequence per read     (bwa.cpp:190-230)
+ *   bsq_align_batch                    <- BwaIndex::align_sequence per read     (bwa.cpp:141-181)
  *                                         = mem_align1 + mem_reg2aln for a whole cursor batch
  *   bsq_render_tsv                     <- the BwaMatch rendering of align_sequence
  *                                         (extract_reference_subseq, cigar_compressed_to_string)
@@ -54,7 +54,7 @@ typedef struct bsq_batch bsq_batch;
 /* One alignment region = one bwa_result row (bioseqdb--0.0.0.sql:196-212).  Coordinates are the
  * reference's: rb/re in the forward+reverse space [0, 2*l_pac) (Q6). */
 typedef struct {
-    int64_t ref_id;            /* anns[rid].name reinterpreted as int64 (bwa.cpp:209) */
+    int64_t ref_id;            /* anns[rid].name reinterpreted as int64 (bwa.cpp:160) */
     int64_t rb, re;            /* mem_alnreg_t rb/re */
     int32_t ref_match_start;   /* (int32)(rb - anns[rid].offset)  */
     int32_t ref_match_end;     /* (int32)(re - anns[rid].offset)  */

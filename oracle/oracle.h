@@ -10,6 +10,8 @@
  *     published BWA-MEM 0.7.x sources (bwt.c, bwamem.c, ksw.c, bntseq.c, bwa.c, kbtree.h,
  *     ksort.h) as written down in SURVEY.md Appendix A.
  *
+ * Attribution: restates BWA (lh3/bwa, Apache License 2.0) and klib (MIT License); see NOTICE.
+ *
  * Parity status: the reference's own tests (test/run.py) pin nothing on the alignment path and
  * ship no golden vectors, and libbwa cannot be built here.  The oracle is pinned by brute-force
  * cross-checks (FM counts, SMEMs, full-matrix DP) and planted-truth known-answer tests under

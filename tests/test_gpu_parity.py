@@ -112,7 +112,7 @@ def test_parity_retry_path_tiny_caps(monkeypatch):
 def test_parity_smem_list_spill(monkeypatch):
     """Two SMEM list entries per lane in LDS: nearly every bwt_smem1 list continues in the read's global
     spill area.  The ring-window guard of the extension and the k-mer table stay on."""
-    monkeypatch.setenv("BSQ_LCAP", "2")
+    monkeypatch.setenv("BSQ_TEST_LCAP", "2")
     ref = synth.make_reference(2_000_000, n_run_every=500_000, n_run_len=300, dup_frac=0.02)
     reads = synth.make_reads(ref, 1500, seed=29)
     pi, oi = build_pair([t.decode() for t in ref.texts()])

@@ -45,7 +45,7 @@ def test_empty_reference_returns_no_rows_and_no_lrand48_call():
     q = NucleotideSequence.from_text("ACGT" * 40)
     assert nuclseq_search_bwa(q, []) == []
     assert nuclseq_multi_search_bwa([(1, q), (2, q)], [(1, NucleotideSequence.from_text(""))]) == []
-    assert lrand48_calls() == 5   # align_sequence returns before mem_align1 (bwa.cpp:191)
+    assert lrand48_calls() == 5   # align_sequence returns before mem_align1 (bwa.cpp:142-143)
 
 
 def test_result_columns():

@@ -1,5 +1,5 @@
 """bwa_result rendering on the host (no GPU): the multi-threaded renderer gives the
-same text as one thread, and ref_subseq follows extract_reference_subseq's quirks (bwa.cpp:104-117):
+same text as one thread, and ref_subseq follows extract_reference_subseq's quirks (bwa.cpp:55-68):
 hole symbols overlaid at row-relative offsets on the concatenated text (Q3), later holes win."""
 import ctypes
 import random
