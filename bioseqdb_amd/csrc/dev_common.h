@@ -102,6 +102,18 @@ DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
     return w;
 }
 
+// ksw_global2 on an n x n problem (bwa_gen_cigar2 with l_query == rlen) whose gapless diagonal scores
+// `diag`: every other path through the band has g >= 1 insertions and as many deletions, so it scores at
+// most (n - g)*mat_max - (o_ins + g*e_ins) - (o_del + g*e_del) <= (n-1)*mat_max - oe_ins - oe_del.  When
+// the diagonal beats that bound strictly, every diagonal cell's M is strictly above its E and F (an E/F
+// path to (i,i) completed along the diagonal would reach the bound), so the DP's traceback bits there are
+// all 0, the walk from (n-1, n-1) is n diagonal steps and eh[qlen].x == diag, for any band w >= 0: the
+// result is "nM" with score `diag`, exactly what the DP returns, so the DP is skipped.
+DEV bool diagonal_wins(const DOpts &o, int n, int diag)
+{
+    const int64_t bound = (int64_t)(n - 1) * o.mat_max - (o.o_ins + o.e_ins) - (o.o_del + o.e_del);
+    return (int64_t)diag > bound;
+}
 
 // Sequential reader of the target bases target(i) = ref_at(start + dir*i), i = 0, 1, 2, ...: keeps the
 // current and the next 16-base pac word in registers so the per-row base never waits on memory.

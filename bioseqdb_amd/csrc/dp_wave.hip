@@ -291,14 +291,17 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
     const bool rev = rb >= ix.l_pac;
     QW qa{q_off, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
     TAcc ta{&ix, rev ? re - 1 : rb, rev ? -1 : 1};
-    if (l_query == rlen && w_ == 0) {
+    int s = 0;
+    if (l_query == rlen) {
+        const Score sc = score_of(o);
+        for (int i = lane_id(); i < l_query; i += 64) s += sc(ta(i), qa(i));
+        s = wave_sum(s);
+    }
+    if (l_query == rlen && (w_ == 0 || diagonal_wins(o, l_query, s))) {
         if (cap < 1) { ovf = true; return 0; }
         cig[0] = (uint32_t)l_query << 4;
         *ncig = 1;
-        int s = 0;
-        const Score sc = score_of(o);
-        for (int i = lane_id(); i < l_query; i += 64) s += sc(ta(i), qa(i));
-        *score = wave_sum(s);
+        *score = s;
     } else {
         int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
         int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
@@ -569,16 +572,19 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
     const int64_t t_start = rev ? re - 1 : rb;
     const int t_dir = rev ? -1 : 1;
     const Score sc = score_of(o);
-    if (l_query == rlen && w_ == 0) {
-        if (cap < 1) { ovf = true; return 0; }
-        bases += (uint64_t)((rlen + 3) >> 2);
-        cig[0] = (uint32_t)l_query << 4;
-        *ncig = 1;
+    if (l_query == rlen) {
         int sum = 0;
         for (int i = gl; i < l_query; i += G)
             sum += sc(ref_at(ix, t_start + (int64_t)t_dir * i), g_lds_dp[q_off + q_start + q_dir * i]);
-        *score = grp_sum<G>(sum);
-        return 1;
+        sum = grp_sum<G>(sum);
+        if (w_ == 0 || diagonal_wins(o, l_query, sum)) {
+            if (cap < 1) { ovf = true; return 0; }
+            bases += (uint64_t)((rlen + 3) >> 2);
+            cig[0] = (uint32_t)l_query << 4;
+            *ncig = 1;
+            *score = sum;
+            return 1;
+        }
     }
     int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
     int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);

@@ -272,6 +272,38 @@ def test_ksw_global2_vs_full_matrix():
         assert cigar_score(list(cig)[:n.value], q, t, od, ed, oi_, ei) == sc
 
 
+def test_diagonal_shortcut_theorem():
+    """dev_common.h diagonal_wins(): for an n x n ksw_global2 whose gapless diagonal scores above
+    (n-1)*mat_max - oe_ins - oe_del, the DP (oracle, full traceback) returns exactly "nM" with the
+    diagonal's score, for every band.  The reg2aln kernels skip the DP on that predicate."""
+    rng = random.Random(12)
+    mat_max = max(MAT)
+    hits = 0
+    for trial in range(3000):
+        n = rng.choice([1, 2, 3, 5, 8, 20, 60, 150])
+        t = [rng.randrange(4) for _ in range(n)]
+        q = list(t)
+        for _ in range(rng.choice([0, 1, 1, 2, 2, 3, 4])):
+            k = rng.randrange(n)
+            q[k] = rng.randrange(5) if rng.random() < 0.2 else (q[k] + rng.randint(1, 3)) % 4
+        if rng.random() < 0.3 and n > 8:   # low-complexity stretches: off-diagonal paths score well
+            s = rng.randrange(n - 4)
+            for k in range(s, min(n, s + rng.randint(3, 12))):
+                t[k] = q[k] = t[s]
+        od, ed, oi_, ei = rng.choice([(6, 6, 1, 1), (6, 1, 6, 1), (3, 2, 4, 1), (0, 1, 0, 1), (1, 0, 0, 1)])
+        diag = sum(MAT[t[i] * 5 + q[i]] for i in range(n))
+        if diag <= (n - 1) * mat_max - (oi_ + ei) - (od + ed):
+            continue
+        hits += 1
+        for w in (0, 1, 3, 8, 100):
+            nc = ctypes.c_int()
+            cig = (ctypes.c_uint32 * 512)()
+            sc = O.lib().orc_ksw_global2(n, bytes(q), n, bytes(t), MAT, od, ed, oi_, ei, w, ctypes.byref(nc), cig, 512)
+            assert sc == diag, (trial, w)
+            assert list(cig)[:nc.value] == [n << 4], (trial, w, list(cig)[:nc.value])
+    assert hits > 1000
+
+
 # ------------------------------------------------------------------------------- planted reads (KAT)
 def test_planted_reads():
     rng = random.Random(6)
