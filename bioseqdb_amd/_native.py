@@ -121,6 +121,14 @@ SIGNATURES = {
     "bsq_batch_render_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "bsq_fasta_parse": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
+    "bsq_index_device_tables": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), _P, ctypes.c_int]),
+    "bsq_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
+    "bsq_group_free": (None, [_P]),
+    "bsq_group_size": (ctypes.c_int, [_P]),
+    "bsq_group_replicate": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_double)]),
+    "bsq_group_run": (ctypes.c_int, [_P, ctypes.POINTER(Opts), _P, ctypes.c_int32, ctypes.c_uint64]),
+    "bsq_group_hits": (ctypes.POINTER(Hits), [_P]),
+    "bsq_group_render_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
 }
 
 _lib = None

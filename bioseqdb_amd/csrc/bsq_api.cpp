@@ -106,6 +106,8 @@ static void set_err(const char *fmt, ...)
     } while (0)
 
 extern "C" const char *bsq_last_error(void) { return g_err.c_str(); }
+// for the other translation units of the library (group.cpp); not part of include/bsq.h
+extern "C" void bsq_internal_set_error(const char *msg) { g_err = msg ? msg : ""; }
 extern "C" const char *bsq_version(void) { return "bsq 0.1 (gfx950)"; }
 extern "C" void bsq_free(void *p) { free(p); }
 
@@ -532,6 +534,19 @@ extern "C" int bsq_index_layout(const bsq_index *idx, uint64_t *bytes, void *met
         if (!h.holes.empty()) memcpy(p, h.holes.data(), h.holes.size() * sizeof(Hole));
     }
     *meta_bytes = need;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_device_tables(const bsq_index *idx, int *device, bsq_table *tables, int n_tables)
+{
+    if (!idx || !idx->h.built || !idx->h.dev || !tables || n_tables != BSQ_N_TABLES) {
+        set_err("index not on a device / invalid argument"); return BSQ_E_INVALID;
+    }
+    const DeviceIndex *d = idx->h.dev;
+    const IndexMeta m = meta_of(idx->h);
+    void *cur[T_N] = {d->occ, d->occ32, d->sa, d->pac, d->ann_off, d->ann_id, d->ann_len, d->kmer};
+    for (int t = 0; t < T_N; ++t) tables[t] = bsq_table{m.table_bytes[t] ? cur[t] : nullptr, m.table_bytes[t]};
+    if (device) *device = d->device;
     return BSQ_OK;
 }
 

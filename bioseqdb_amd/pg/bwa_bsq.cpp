@@ -49,7 +49,10 @@ void BwaRows::cigar_text(int64_t k, std::string &out) const
     }
 }
 
-BwaIndex::BwaIndex(int dev) : options(new BsqMemOpt()), index_(nullptr), device_(dev)
+BwaIndex::BwaIndex(int dev) : BwaIndex(std::vector<int>{dev}) {}
+
+BwaIndex::BwaIndex(const std::vector<int> &devices)
+    : options(new BsqMemOpt()), index_(nullptr), devices_(devices.empty() ? std::vector<int>{0} : devices)
 {
     const int rc = bsq_index_create(&index_);
     if (rc != BSQ_OK) {
@@ -59,11 +62,12 @@ BwaIndex::BwaIndex(int dev) : options(new BsqMemOpt()), index_(nullptr), device_
 }
 
 BwaIndex::BwaIndex(BwaIndex &&o) noexcept
-    : options(o.options), index_(o.index_), device_(o.device_), batch_(o.batch_), batch_reads_(o.batch_reads_),
-      batch_bases_(o.batch_bases_), rows_(std::move(o.rows_))
+    : options(o.options), index_(o.index_), devices_(o.devices_), group_(o.group_), batch_(o.batch_),
+      batch_reads_(o.batch_reads_), batch_bases_(o.batch_bases_), rows_(std::move(o.rows_))
 {
     o.options = nullptr;
     o.index_ = nullptr;
+    o.group_ = nullptr;
     o.batch_ = nullptr;
 }
 
@@ -71,6 +75,7 @@ BwaIndex::~BwaIndex()
 {
     rows_ = BwaRows();
     bsq_batch_free(batch_);
+    bsq_group_free(group_);
     bsq_index_free(index_);
     delete options;
 }
@@ -84,14 +89,14 @@ int32_t BwaIndex::n_refs() const { return bsq_index_n_refs(index_); }
 void BwaIndex::build()
 {
     if (empty()) return;   // bwa.cpp:108-109
-    if (bsq_device_count() > device_) check(bsq_index_build_device(index_, device_));
+    if (bsq_device_count() > device()) check(bsq_index_build_device(index_, device()));
     else check(bsq_index_build(index_, 0));   // same tables; aligning then reports the missing device
 }
 
 void BwaIndex::ensure_batch(int32_t n, int64_t bases) const
 {
     if (batch_ && batch_reads_ >= n && batch_bases_ >= bases) return;
-    check(bsq_index_upload(index_, device_));   // no-op for an index built on the device
+    check(bsq_index_upload(index_, device()));   // no-op for an index built on the device
     rows_ = BwaRows();
     bsq_batch_free(batch_);
     batch_ = nullptr;
@@ -101,6 +106,21 @@ void BwaIndex::ensure_batch(int32_t n, int64_t bases) const
     check(bsq_batch_create(index_, std::max(r, 1), std::max<int64_t>(b, 1), &batch_));
     batch_reads_ = std::max(r, 1);
     batch_bases_ = std::max<int64_t>(b, 1);
+}
+
+void BwaIndex::ensure_group() const
+{
+    if (group_) return;
+    check(bsq_index_upload(index_, device()));   // no-op for an index built on the first device
+    bsq_group *g = nullptr;
+    check(bsq_group_create(devices_.data(), (int)devices_.size(), &g));
+    const int rc = bsq_group_replicate(g, index_, nullptr);   // one build, broadcast over xGMI
+    if (rc != BSQ_OK) {
+        const std::string m = bsq_last_error();
+        bsq_group_free(g);
+        throw BsqFailure(rc, m);
+    }
+    group_ = g;
 }
 
 const BwaRows &BwaIndex::align_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
@@ -120,18 +140,25 @@ const BwaRows &BwaIndex::align_rows(const NucleotideSequence *const *seqs, int32
     }
     int64_t bases = 0;
     for (int32_t i = 0; i < n; ++i) bases += ns_len(seqs[i]);
-    ensure_batch(n, bases);
     const void *const *ptrs = reinterpret_cast<const void *const *>(seqs);
     const bsq_opts o = (opts ? *opts : *options).c_abi();
     uint64_t &calls = bsq_backend_lrand48_calls();
-    check(bsq_batch_set_nuclseqs(batch_, ptrs, n));
-    check(bsq_batch_run(batch_, &o, calls));
+    if (devices_.size() > 1) {   // the fetch spread over the group, member k taking a contiguous share
+        ensure_group();
+        check(bsq_group_run(group_, &o, ptrs, n, calls));
+        rows_.view_ = bsq_group_hits(group_);
+    } else {
+        ensure_batch(n, bases);
+        check(bsq_batch_set_nuclseqs(batch_, ptrs, n));
+        check(bsq_batch_run(batch_, &o, calls));
+        rows_.view_ = bsq_batch_hits(batch_);
+    }
     calls += (uint64_t)n;
-    rows_.view_ = bsq_batch_hits(batch_);
     if (nuclseq_columns && rows_.view_->n_hits > 0) {
         uint8_t *cols = nullptr;
         int64_t *off = nullptr;
-        check(bsq_batch_render_nuclseqs(batch_, ptrs, &cols, &off));
+        check(group_ ? bsq_group_render_nuclseqs(group_, ptrs, &cols, &off)
+                     : bsq_batch_render_nuclseqs(batch_, ptrs, &cols, &off));
         rows_.cols_.reset(cols);
         rows_.col_off_.reset(off);
     }
@@ -228,7 +255,7 @@ std::shared_ptr<BwaIndex> BwaIndexCache::get_or_build(const RefDigest &d, std::s
     const size_t cap = e ? (size_t)std::max(0, atoi(e)) : 2;
     std::lock_guard<std::mutex> lk(mu_);
     for (auto it = lru_.begin(); it != lru_.end(); ++it) {
-        if (it->d == d && it->device == fresh->device()) {
+        if (it->d == d && it->devices == fresh->devices()) {
             lru_.splice(lru_.begin(), lru_, it);
             ++hits_;
             return lru_.front().idx;
@@ -237,7 +264,7 @@ std::shared_ptr<BwaIndex> BwaIndexCache::get_or_build(const RefDigest &d, std::s
     fresh->build();
     ++builds_;
     if (cap) {
-        lru_.push_front(Entry{d, fresh->device(), fresh});
+        lru_.push_front(Entry{d, fresh->devices(), fresh});
         while (lru_.size() > cap) lru_.pop_back();
     }
     return fresh;

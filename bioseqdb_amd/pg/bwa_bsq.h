@@ -9,6 +9,8 @@
 //   * BwaIndexCache               the index of a reference cursor kept across calls (the reference rebuilds
 //                                 it on every call, Q13: extension.cpp:326,359), keyed by a digest of the
 //                                 rows' ids and nuclseq bytes;
+//   * several devices             BwaIndex({0, 1, ...}) aligns each batch over a bsq_group (one process, one
+//                                 RCCL communicator per GPU, the index broadcast once);
 //   * failures                    libbwa never fails; libbsq can (no device, HIP error, a read beyond every
 //                                 retry capacity).  They surface as BsqFailure, which the fmgr layer turns into
 //                                 ereport(ERROR) only after every C++ object is released (extension_bsq.cpp).
@@ -83,6 +85,7 @@ private:
 class BwaIndex {
 public:
     explicit BwaIndex(int device = 0);
+    explicit BwaIndex(const std::vector<int> &devices);   // several: a bsq_group over them
     ~BwaIndex();
     BwaIndex(BwaIndex &&o) noexcept;
     BwaIndex(const BwaIndex &) = delete;
@@ -102,14 +105,17 @@ public:
 
     bool empty() const;          // no reference bases: align_* return no rows and draw no lrand48 value
     int32_t n_refs() const;
-    int device() const { return device_; }
+    int device() const { return devices_[0]; }
+    const std::vector<int> &devices() const { return devices_; }
 
     BsqMemOpt *options;          // bwa.h:41 (mem_opt_t* there)
 
 private:
     void ensure_batch(int32_t n, int64_t bases) const;
+    void ensure_group() const;
     bsq_index *index_;
-    int device_;
+    std::vector<int> devices_;
+    mutable bsq_group *group_ = nullptr;
     mutable bsq_batch *batch_ = nullptr;
     mutable int32_t batch_reads_ = 0;
     mutable int64_t batch_bases_ = 0;
@@ -133,14 +139,14 @@ struct RefDigest {
 class BwaIndexCache {
 public:
     static BwaIndexCache &backend();
-    // The cached index for (digest, device), or `fresh` after building it (and caching it).
+    // The cached index for (digest, devices), or `fresh` after building it (and caching it).
     std::shared_ptr<BwaIndex> get_or_build(const RefDigest &d, std::shared_ptr<BwaIndex> fresh);
     void clear();
     size_t hits() const { return hits_; }
     size_t builds() const { return builds_; }
 
 private:
-    struct Entry { RefDigest d; int device; std::shared_ptr<BwaIndex> idx; };
+    struct Entry { RefDigest d; std::vector<int> devices; std::shared_ptr<BwaIndex> idx; };
     std::list<Entry> lru_;
     std::mutex mu_;
     size_t hits_ = 0, builds_ = 0;

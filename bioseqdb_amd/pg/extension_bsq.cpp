@@ -114,7 +114,22 @@ long env_long(const char *name, long dflt, long lo)
     const char *e = getenv(name);
     return e && *e ? std::max(lo, atol(e)) : dflt;
 }
-int backend_device() { return (int)env_long("BSQ_DEVICE", 0, 0); }
+// BSQ_DEVICES="0,1,2,3": the backend aligns over a group of GPUs (bsq_group); else the one BSQ_DEVICE
+std::vector<int> backend_devices()
+{
+    std::vector<int> d;
+    if (const char *e = getenv("BSQ_DEVICES")) {
+        for (const char *p = e; *p;) {
+            char *end = nullptr;
+            const long v = strtol(p, &end, 10);
+            if (end == p) { ++p; continue; }
+            if (v >= 0) d.push_back((int)v);
+            p = end;
+        }
+    }
+    if (d.empty()) d.push_back((int)env_long("BSQ_DEVICE", 0, 0));
+    return d;
+}
 long query_fetch_rows() { return env_long("BSQ_FETCH_ROWS", 1L << 18, 1); }
 constexpr long kRefFetchRows = 64;   // reference rows are long; their bytes are copied by add_ref_sequence
 
@@ -198,7 +213,7 @@ struct CallIndex {
 CallIndex index_from_query(const char *sql, HeapTupleHeader opts, Oid nuclseq_oid)
 {
     const auto t0 = std::chrono::steady_clock::now();
-    auto fresh = std::make_shared<BwaIndex>(backend_device());
+    auto fresh = std::make_shared<BwaIndex>(backend_devices());
     RefDigest digest;
     for_each_fetch(sql, nuclseq_oid, kRefFetchRows, [&](const std::vector<int64_t> &ids,
                                                        const std::vector<const NucleotideSequence *> &seqs) {

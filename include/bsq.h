@@ -156,6 +156,36 @@ int bsq_index_upload_into(bsq_index *idx, int device, const bsq_table *tables, i
  * broadcast), described by its metadata blob.  Aligns and renders like the original. */
 int bsq_index_import(const void *meta, uint64_t meta_bytes, int device, const bsq_table *tables, int n_tables,
                      bsq_index **out);
+/* Borrowed device pointers and sizes of an uploaded (or device-built) index's tables and its device: the
+ * source buffers of a broadcast. */
+int bsq_index_device_tables(const bsq_index *idx, int *device, bsq_table *tables, int n_tables);
+
+/* ---- One process driving several devices (the Postgres backend is a single
+ * process, so `bsq_index_upload(idx, devices[], n)` becomes a group).  Replaces the per-read loop of
+ * nuclseq_multi_search_bwa (extension.cpp:362-370) spread over n GPUs. ---- */
+typedef struct bsq_group bsq_group;
+/* One RCCL communicator per device (ncclCommInitAll over xGMI) and one host worker per member.  A device
+ * listed twice makes a group of replicas on one GPU: valid (tests use it), replication then copies device to
+ * device instead of using RCCL. */
+int bsq_group_create(const int *devices, int n_devices, bsq_group **out);
+void bsq_group_free(bsq_group *g);
+int bsq_group_size(const bsq_group *g);
+/* Puts a built index on every member: uploaded to (or built on) the first member's device if it is not there
+ * yet, then every device table broadcast from it (ncclBroadcast inside one ncclGroupStart/End) and imported on
+ * the others.  The group keeps the replicas until the next replicate or free; `idx` must outlive the group's
+ * use of it (member 0 aligns on it).  *broadcast_ms: wall time of the broadcast (NULL: not reported). */
+int bsq_group_replicate(bsq_group *g, bsq_index *idx, double *broadcast_ms);
+/* Aligns n_reads nuclseq reads over the members: member k takes reads [k*n/G, (k+1)*n/G) with lrand48
+ * positions from first_call_seq + its first read (identical rows to one device aligning all reads in
+ * order, Q10/Q16).  Every member runs on its own host thread and copies its records to the host over its
+ * own PCIe link; the merged view (read order, batch-wide read_index and cigar_off) is borrowed until the
+ * next run or free.  With reads == NULL the members re-run the reads staged by the previous call. */
+int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                  uint64_t first_call_seq);
+const bsq_hits *bsq_group_hits(const bsq_group *g);
+/* build_tuple_bwa's two nuclseq columns of the last run's rows, rendered on every member for its shard
+ * (layout as bsq_batch_render_nuclseqs, rows in the merged order).  `reads` as given to bsq_group_run. */
+int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads, uint8_t **out, int64_t **out_off);
 
 /* ---- alignment --------------------------------------------------------------------------------- */
 /* Value of the (pos+1)-th lrand48() call of an unseeded glibc/musl process (Q10). */

@@ -59,3 +59,55 @@ def test_gather_records_world2_gloo():
 
 def test_merge_rows():
     assert D.merge_rows([[(1,), (2,)], [], [(3,)]]) == [(1,), (2,), (3,)]
+
+
+def _protocol_worker(rank, world, port, q):
+    """The multi-process protocol of bench.py --gpus N / dist.py with the oracle standing in for the GPU aligner:
+    shard the reads, align the shard from its own lrand48 position, gather the rows to rank 0."""
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(__file__))
+    import oracle_py as O
+    from parity_util import _oracle_batch_tsv
+    from bioseqdb_amd import NucleotideSequence, effective_opts, synth
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ref = synth.make_reference(120_000, n_rows=2, n_run_every=50_000, n_run_len=80)
+    reads = synth.make_reads(ref, 301, seed=3)
+    oi = O.OracleIndex()
+    for i, t in enumerate(ref.texts()):
+        oi.add_ref(i + 1, O.Nuclseq(t.decode()).raw)
+    oi.build()
+    oo = O.opts_from(effective_opts(None, 2))
+    raws = [NucleotideSequence.from_text(reads.text(i)).raw for i in range(reads.n)]
+    base = 1000   # this backend's lrand48 position before the call
+    lo, hi = D.shard(reads.n, rank, world)
+    text, counts = _oracle_batch_tsv(oi, oo, raws[lo:hi], D.first_call_of(rank, world, reads.n, base), threads=1)
+    rec = np.frombuffer(np.array(counts, dtype=np.int64).tobytes() + text.encode("latin-1"), dtype=np.uint8)
+    got = D.gather_records(rec)
+    whole = _oracle_batch_tsv(oi, oo, raws, base, threads=2) if rank == 0 else None
+    q.put((rank, [g.tobytes() for g in got], whole, [D.shard(reads.n, r, world) for r in range(world)]))
+    dist.destroy_process_group()
+
+
+def test_sharded_protocol_equals_one_backend_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_protocol_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, parts, (whole_text, whole_counts), shards = res[0]
+    assert len(parts) == world and all(r[1] == [] for r in res[1:])
+    text, counts = "", []
+    for buf, (lo, hi) in zip(parts, shards):
+        c = np.frombuffer(buf[:8 * (hi - lo)], dtype=np.int64).tolist()
+        counts += c
+        text += buf[8 * (hi - lo):].decode("latin-1")
+    assert counts == whole_counts                  # rows per read, read order
+    assert text == whole_text and len(text) > 1000  # identical rows: lrand48 positions continue across ranks

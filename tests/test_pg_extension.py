@@ -283,3 +283,23 @@ def test_single_search_query_id_null(stub, world):
         _check_rows(got, exp)
     assert stub.pgstub_lrand48_calls() == k
     assert stub.pgstub_index_cache_builds() == 1
+
+
+@pytest.mark.gpu
+def test_multi_search_over_a_device_group(stub, world, monkeypatch):
+    """BSQ_DEVICES lists several GPUs: each SPI fetch is aligned over a bsq_group (index broadcast once, reads
+    sharded over the members, rows merged in read order).  The box has one GPU, so the group holds three
+    replicas on it; rows, nuclseq columns and the lrand48 stream must not change."""
+    ref_rows, oi, q = world
+    db = Db(stub)
+    db.table("refs", ref_rows)
+    db.table("reads", q[:900])
+    monkeypatch.setenv("BSQ_DEVICES", "0,0,0")
+    monkeypatch.setenv("BSQ_FETCH_ROWS", "301")
+    stub.pgstub_set_lrand48_calls(99)
+    got, err = db.call("reads", "refs")
+    assert err is None, err
+    exp, k = _expected(oi, 3, None, q[:900], 99)
+    _check_rows(got, exp)
+    assert stub.pgstub_lrand48_calls() == k
+    assert stub.pgstub_live_allocs() == 0
