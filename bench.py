@@ -488,6 +488,7 @@ def main() -> int:
         },
         "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
         "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
+        "stages_work": {names[i]: float(stage_work[i]) for i in range(6)},
         "index_build_s": round(t_build, 2),
         "index_build": args.index_build,
         "index_upload_s": round(t_upload, 2),

@@ -660,6 +660,7 @@ struct EhL {   // offset-based so the accesses stay in the LDS address space (ds
     DEV void set(int j, int2 v) const { g_lds_eh[base + j * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
+#define EXT_LDS_COLS 64   // ring columns (a power of two)
 // 64-column ring of u16 pairs in LDS (column j at slot j & 63, lane-interleaved): ksw_extend2 only touches
 // columns [beg, end] of the current row and beg never decreases, so the ring holds every live column while
 // the window stays under 64 columns; columns are given their initial value when the band first reaches
@@ -668,8 +669,8 @@ struct EhRing {
     static constexpr bool kRing = true;
     bool *ovf;
     int base;
-    DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + (j & 63) * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
-    DEV void set(int j, int2 v) const { g_lds_eh[base + (j & 63) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
+    DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
+    DEV void set(int j, int2 v) const { g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
 template <class EH, class QA>
@@ -684,7 +685,7 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
     // eh[0] = h0, eh[1] = max(h0 - oe_ins, 0), eh[j>=2] = eh[j-1] - e_ins while eh[j-1] > e_ins, else 0
     const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
     auto init_h = [&](int jj) { return jj == 0 ? h0 : (jj == 1 ? v1 : (v1 - (jj - 1) * e_ins > 0 ? v1 - (jj - 1) * e_ins : 0)); };
-    int hi = EH::kRing ? (qlen < 63 ? qlen : 63) : qlen;   // columns <= hi hold their values
+    int hi = EH::kRing ? (qlen < EXT_LDS_COLS - 1 ? qlen : EXT_LDS_COLS - 1) : qlen;   // columns <= hi hold their values
     for (j = 0; j <= hi; ++j) eh.set(j, make_int2(init_h(j), 0));
     max = o.mat_max > 0 ? o.mat_max : 0;
     max_ins = (int)((double)(qlen * max + end_bonus - o_ins) / e_ins + 1.);
@@ -709,7 +710,7 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
             if (h1 < 0) h1 = 0;
         } else h1 = 0;
         if (EH::kRing && end > hi) {   // materialise the columns the band reaches for the first time
-            if (end - beg >= 63) { *eh.ovf = true; break; }
+            if (end - beg >= EXT_LDS_COLS - 1) { *eh.ovf = true; break; }
             for (j = hi + 1; j <= end; ++j) eh.set(j, make_int2(init_h(j), 0));
             hi = end;
         }
@@ -1103,7 +1104,6 @@ struct QMakeL {
 
 // Extension rows for k_extend<true>: the eh row is a 64-column LDS ring (EhRing); the read is staged
 // in LDS once per read (QMakeL) after the ring columns.
-#define EXT_LDS_COLS 64
 struct EhSmall {
     int lane;       // LDS column (threadIdx.x of the 64-thread block)
     bool *ovf;      // ring overflow -> read re-run by the retry pass
@@ -1280,6 +1280,9 @@ DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg 
 
 DEV void permute(ExtCtx &X, int n)
 {
+    bool ident = true;   // most region lists are already in order: skip the two copies through scratch
+    for (int i = 0; i < n; ++i) ident = ident && X.idx[i] == i;
+    if (ident) return;
     for (int i = 0; i < n; ++i) X.tmp[i] = X.av[X.idx[i]];
     for (int i = 0; i < n; ++i) X.av[i] = X.tmp[i];
 }
