@@ -323,47 +323,137 @@ static void gen_cnt_table(orc_index *b)
 
 /* Fill bwt_t from T and its SA: is_bwt ($-removed BWT + primary), bwt packing (bwa.cpp:48-50),
  * bwt_bwtupdate_core (occ interleave every 128), bwt_cal_sa(32) (sampled true SA, sa[0] = -1). */
+/* BWT of T$ from its suffix array and libbwa's interleaved occ layout (bwt_bwtupdate_core), on up to 16 POSIX
+ * threads: a 3 Gbp text has 6e9 rows (bench.py --config c4 builds its CPU-baseline index this way). */
+typedef struct {
+    const uint8_t *T; const int64_t *sa64; const void *sa_ext; int sa_bytes;
+    uint64_t n, lo, hi, primary, found, bad;   /* rows [lo, hi) / words [lo, hi) */
+    uint32_t *raw, *buf; uint64_t cnt[4];
+} bwt_job;
+
+static uint64_t sa_at(const bwt_job *j, uint64_t r)
+{
+    return j->sa64 ? (uint64_t)j->sa64[r] : (j->sa_bytes == 4 ? (uint64_t)((const uint32_t *)j->sa_ext)[r]
+                                                               : ((const uint64_t *)j->sa_ext)[r]);
+}
+
+static void *bwt_find_primary(void *a)
+{
+    bwt_job *j = a;
+    j->found = (uint64_t)-1; j->bad = 0;
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        const uint64_t s = sa_at(j, i);
+        if (s > j->n) j->bad = 1;
+        else if (s == 0) j->found = i;
+    }
+    return NULL;
+}
+
+static void *bwt_fill_words(void *a)   /* raw word w holds BWT characters 16w .. 16w+15 ($ row skipped) */
+{
+    bwt_job *j = a;
+    for (uint64_t w = j->lo; w < j->hi; ++w) {
+        uint32_t v = 0;
+        for (uint64_t t = 0; t < 16; ++t) {
+            const uint64_t pos = 16 * w + t;
+            if (pos >= j->n) break;
+            const uint64_t row = pos + (pos >= j->primary);
+            v |= (uint32_t)j->T[sa_at(j, row) - 1] << ((15 - t) << 1);
+        }
+        j->raw[w] = v;
+    }
+    return NULL;
+}
+
+static void *bwt_count(void *a)   /* per-thread base counts over characters [lo, hi) (multiples of 128) */
+{
+    bwt_job *j = a;
+    memset(j->cnt, 0, sizeof j->cnt);
+    for (uint64_t i = j->lo; i < j->hi; ++i) ++j->cnt[j->raw[i >> 4] >> ((~i & 0xf) << 1) & 3];
+    return NULL;
+}
+
+static void *bwt_interleave(void *a)   /* occ block b = counts before it (8 words) + its 8 BWT words */
+{
+    bwt_job *j = a;
+    uint64_t c[4] = {j->cnt[0], j->cnt[1], j->cnt[2], j->cnt[3]};
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        uint64_t k = (i >> 7) * 16 + ((i & 127) >> 4) + 8;
+        if (i % 128 == 0) memcpy(j->buf + (i >> 7) * 16, c, 32);
+        if (i % 16 == 0) j->buf[k] = j->raw[i / 16];
+        ++c[j->raw[i >> 4] >> ((~i & 0xf) << 1) & 3];
+    }
+    return NULL;
+}
+
+static void run_jobs(bwt_job *jobs, int nt, void *(*fn)(void *))
+{
+    pthread_t th[16];
+    for (int t = 1; t < nt; ++t) pthread_create(&th[t], NULL, fn, &jobs[t]);
+    fn(&jobs[0]);
+    for (int t = 1; t < nt; ++t) pthread_join(th[t], NULL);
+}
+
 static int finish_bwt(orc_index *idx, const uint8_t *T, uint64_t n, const int64_t *sa64, const void *sa_ext, int sa_bytes)
 {
-    uint64_t i, k, c[4];
-#define SA_AT(r) (sa64 ? (uint64_t)sa64[r] : (sa_bytes == 4 ? (uint64_t)((const uint32_t *)sa_ext)[r] : ((const uint64_t *)sa_ext)[r]))
+    uint64_t i, c[4];
+    const int nt = n < (1u << 20) ? 1 : 16;
+    bwt_job jobs[16];
+    for (int t = 0; t < nt; ++t) {
+        memset(&jobs[t], 0, sizeof jobs[t]);
+        jobs[t].T = T; jobs[t].sa64 = sa64; jobs[t].sa_ext = sa_ext; jobs[t].sa_bytes = sa_bytes; jobs[t].n = n;
+    }
     idx->seq_len = n;
     idx->bwt_size = (n + 15) >> 4;
-    uint32_t *raw = calloc(idx->bwt_size + 1, 4);
-    uint64_t primary = (uint64_t)-1, j = 0;
-    for (i = 0; i <= n; ++i) {
-        uint64_t s = SA_AT(i);
-        if (s > n) { free(raw); return -1; }
-        if (s == 0) { primary = i; continue; }
-        uint8_t ch = T[s - 1];
-        raw[j >> 4] |= (uint32_t)ch << ((15 - (j & 15)) << 1);
-        ++j;
+    /* the $ row (primary): SA[primary] == 0 */
+    for (int t = 0; t < nt; ++t) { jobs[t].lo = (n + 1) * (uint64_t)t / nt; jobs[t].hi = (n + 1) * (uint64_t)(t + 1) / nt; }
+    run_jobs(jobs, nt, bwt_find_primary);
+    uint64_t primary = (uint64_t)-1, nfound = 0;
+    for (int t = 0; t < nt; ++t) {
+        if (jobs[t].bad) return -1;
+        if (jobs[t].found != (uint64_t)-1) { primary = jobs[t].found; ++nfound; }
     }
-    if (primary == (uint64_t)-1 || j != n) { free(raw); return -1; }
+    if (nfound != 1) return -1;
     idx->primary = primary;
+    uint32_t *raw = calloc(idx->bwt_size + 1, 4);
+    for (int t = 0; t < nt; ++t) {
+        jobs[t].raw = raw; jobs[t].primary = primary;
+        jobs[t].lo = idx->bwt_size * (uint64_t)t / nt; jobs[t].hi = idx->bwt_size * (uint64_t)(t + 1) / nt;
+    }
+    run_jobs(jobs, nt, bwt_fill_words);
     /* bwt_bwtupdate_core */
     uint64_t n_occ = (n + 127) / 128 + 1;
     idx->bwt_size += n_occ * 8;
     uint32_t *buf = calloc(idx->bwt_size, 4);
-    c[0] = c[1] = c[2] = c[3] = 0;
-    for (i = k = 0; i < n; ++i) {
-        if (i % 128 == 0) { memcpy(buf + k, c, 32); k += 8; }
-        if (i % 16 == 0) buf[k++] = raw[i / 16];
-        ++c[raw[i >> 4] >> ((~i & 0xf) << 1) & 3];
+    const uint64_t nblk = (n + 127) / 128;
+    for (int t = 0; t < nt; ++t) {
+        jobs[t].buf = buf;
+        jobs[t].lo = nblk * (uint64_t)t / nt * 128; jobs[t].hi = nblk * (uint64_t)(t + 1) / nt * 128;
+        if (jobs[t].hi > n) jobs[t].hi = n;
+        if (jobs[t].lo > n) jobs[t].lo = n;
     }
-    memcpy(buf + k, c, 32);
-    if (k + 8 != idx->bwt_size) { free(raw); free(buf); return -1; }
+    run_jobs(jobs, nt, bwt_count);
+    c[0] = c[1] = c[2] = c[3] = 0;
+    for (int t = 0; t < nt; ++t) {   /* exclusive prefix of the per-thread counts */
+        uint64_t x[4] = {jobs[t].cnt[0], jobs[t].cnt[1], jobs[t].cnt[2], jobs[t].cnt[3]};
+        memcpy(jobs[t].cnt, c, 32);
+        for (int b = 0; b < 4; ++b) c[b] += x[b];
+    }
+    run_jobs(jobs, nt, bwt_interleave);
+    /* the counts after the last (possibly partial) block */
+    const uint64_t fin = (n >> 7) * 16 + ((n & 127) ? 8 + (((n & 127) + 15) >> 4) : 0);
+    if (fin + 8 != idx->bwt_size) { free(raw); free(buf); return -1; }
+    memcpy(buf + fin, c, 32);
     free(raw);
     idx->bwt = buf;
     /* bwt_cal_sa(bwt, 32): samples of the true SA at rows multiple of 32; sa[0] = -1 */
     idx->sa_intv = 32;
     idx->n_sa = (n + 32) / 32;
     idx->sa = calloc(idx->n_sa, 8);
-    for (i = 0; i <= n; i += 32) idx->sa[i / 32] = SA_AT(i);
+    for (i = 0; i <= n; i += 32) idx->sa[i / 32] = sa_at(&jobs[0], i);
     idx->sa[0] = (uint64_t)-1;
     gen_cnt_table(idx);
     idx->built = 1;
-#undef SA_AT
     return 0;
 }
 

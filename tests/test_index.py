@@ -70,3 +70,28 @@ def test_empty_reference_builds_nothing():
     assert pi.l_pac == 0 and lib().bsq_index_seq_len(pi.handle) == 0
     assert pi.align_sequences([NucleotideSequence.from_text("ACGT" * 10)], pi.options or
                               __import__("bioseqdb_amd").effective_opts(None, 2)) == [[]]
+
+
+def test_threaded_bwt_from_sa_equals_host_build():
+    """Texts of >= 2^20 rows take the oracle's 16-thread BWT/occ construction (finish_bwt); its occ counts,
+    primary and sampled SA must equal libbsq's host build, from the oracle's own suffix sort and from
+    libbsq's suffix array (bench.py's C4 CPU-baseline index)."""
+    rng = random.Random(9)
+    rows = ["".join(rng.choice("ACGT") for _ in range(300_001)), "".join(rng.choice("ACGT") for _ in range(262_003))]
+    pi, oi = both(rows)
+    h = pi.handle
+    n = lib().bsq_index_seq_len(h)
+    assert n >= 1 << 20 and n == oi.seq_len and lib().bsq_index_primary(h) == oi.primary
+    eb = ctypes.c_int()
+    sa = lib().bsq_index_sa_data(h, ctypes.byref(eb))
+    o2 = O.OracleIndex()
+    for k, t in enumerate(rows):
+        o2.add_ref(k + 1, NucleotideSequence.from_text(t).raw)
+    o2.build_from_sa(sa, eb.value)
+    assert o2.primary == oi.primary
+    c = (ctypes.c_uint64 * 4)()
+    for k in [-1, 0, 1, 127, 128, n - 129, n - 128, n - 1, n] + [rng.randrange(n) for _ in range(3000)]:
+        assert lib().bsq_index_occ4(h, k, c) == 0
+        assert list(c) == oi.occ4(k) == o2.occ4(k), k
+    for r in [1, 32, 64, n - n % 32] + [32 * rng.randrange(1, n // 32) for _ in range(500)]:
+        assert lib().bsq_index_sa(h, r) == oi.sa(r) == o2.sa(r), r
