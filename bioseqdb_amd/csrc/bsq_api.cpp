@@ -7,6 +7,7 @@
 // with BSQ_E_NODEV.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -84,6 +85,16 @@ hipError_t launch_dec_codes(hipStream_t, const DecView &, const int64_t *, int64
 }  // namespace bsq
 
 using namespace bsq;
+
+// roctx range over a host-side phase (index build / upload, the stage launches of a batch, the record copy):
+// rocprofv3 --marker-trace shows them beside the kernels; without a profiler they cost a call.
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    void next(const char *name) { roctxRangePop(); roctxRangePushA(name); }   // the following phase
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
 
 static thread_local std::string g_err;
 static void set_err(const char *fmt, ...)
@@ -183,6 +194,7 @@ extern "C" int bsq_index_add_ref(bsq_index *idx, int64_t id, const void *nuclseq
 
 extern "C" int bsq_index_build(bsq_index *idx, int threads)
 {
+    Range rg("bsq_index_build");
     if (!idx) { set_err("null index"); return BSQ_E_INVALID; }
     std::string err;
     try {
@@ -337,6 +349,7 @@ static int move_device_tables(bsq_index *idx, int device, const bsq_table *ext)
 // Uploads the host index into its own allocations (ext == nullptr) or into caller-owned buffers.
 static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
 {
+    Range rg("bsq_index_upload");
     if (!idx || !idx->h.built) { set_err("index not built"); return BSQ_E_INVALID; }
     const HostIndex &h = idx->h;
     if (h.dev_built && h.dev) return move_device_tables(idx, device, ext);
@@ -412,6 +425,7 @@ extern "C" int bsq_index_upload(bsq_index *idx, int device) { return upload_impl
 
 extern "C" int bsq_index_build_device(bsq_index *idx, int device)
 {
+    Range rg("bsq_index_build_device");
     if (!idx) { set_err("null index"); return BSQ_E_INVALID; }
     HostIndex &h = idx->h;
     if (h.dev) { set_err("index already uploaded"); return BSQ_E_INVALID; }
@@ -1051,14 +1065,17 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     hipStream_t st = b->stream;
     HIPCHK(hipMemsetAsync(w.status, 0, (size_t)std::max(n, 1) * 4, st));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_SMEM], st));
+    Range rg("smem");
     { const int rc = seed_stage(b, w, o, n, sel); if (rc) return rc; }
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_CHAIN], st));
+    rg.next("chain");
     HIPCHK(launch_chain(w.grid, st, ix, o, w.cp, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.chains, w.seeds, w.n_chains, w.status,
                         w.scratch, b->ctr));
     if (w.sscore)   // long reads: mem_flt_chained_seeds (per read; shorter reads of the batch keep score = len)
         HIPCHK(launch_flt_seeds(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.chains, w.seeds,
                                 w.n_chains, w.status, w.sscore, w.scratch, b->ctr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_EXTEND], st));
+    rg.next("extend");
     const int32_t *order = nullptr;
     if (!sel && w.ekey0 && n > 0) {
         // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
@@ -1070,6 +1087,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,
                          w.n_regs, w.status, w.scratch, b->ctr, order, w.sscore));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
+    rg.next("reg2aln");
     if (!sel && w.cp.max_len <= 1024) {
         // main pass: one wave per read, DP rows across lanes, eh + traceback in LDS (dp_wave.hip)
         const size_t eh_bytes = ((size_t)(w.cp.max_len + 2) * 8 + 15) & ~(size_t)15;
@@ -1150,6 +1168,7 @@ static int grow_pinned(T *&p, int64_t &cap, int64_t need, int64_t keep)
 // batch-wide read indices and CIGAR offsets, read_off[lo .. lo + n] = batch-wide hit offsets.
 static int pack_main(bsq_batch *b, Workspace &w, int n, int lo, int64_t hit_dst, int64_t cig_dst, int64_t tot[2])
 {
+    Range rg("pack+d2h");
     hipStream_t st = b->stream;
     { const int rc = pack_device(b, w, n, true, lo, cig_dst, tot); if (rc) return rc; }
     { int rc = grow_pinned(b->h_pinned, b->h_cap, hit_dst + tot[0], hit_dst); if (rc) return rc; }
@@ -1315,6 +1334,7 @@ static int run_chunk(bsq_batch *b, const DOpts &o, int n, int64_t &hit_total, in
 
 extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_call_seq)
 {
+    Range rg("bsq_batch_run");
     if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
     if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len < 0) {
         set_err("gap extension penalties and max_occ must be positive, min_seed_len nonnegative");
@@ -1478,6 +1498,7 @@ static int pack_seed_chunk(bsq_batch *b, int n)
 
 extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
 {
+    Range rg("bsq_batch_seed");
     if (!b || !opts) { set_err("invalid argument"); return BSQ_E_INVALID; }
     if (opts->max_occ <= 0 || opts->min_seed_len < 0) {
         set_err("max_occ must be positive, min_seed_len nonnegative");

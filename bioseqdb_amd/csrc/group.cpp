@@ -16,6 +16,7 @@
 // Built only on the public C-ABI of bsq_api.cpp plus RCCL.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -192,6 +193,8 @@ extern "C" int bsq_group_replicate(bsq_group *g, bsq_index *idx, double *broadca
         }
     }
     const auto t0 = std::chrono::steady_clock::now();
+    roctxRangePushA("bsq_group_broadcast");
+    struct PopAtExit { ~PopAtExit() { roctxRangePop(); } } pop_at_exit;
     if (G > 1) {
         if (g->rccl) {   // every table from member 0, all broadcasts in one group call
             ncclResult_t r = ncclGroupStart();
