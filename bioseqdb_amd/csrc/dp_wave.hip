@@ -50,6 +50,70 @@ DEV int wave_sum(int v)
     return v;
 }
 
+// Scans over G consecutive lanes (a group; G = 64: the wave), generic shuffles.
+template <int G> DEV int grp_incl_sum(int v, int gl)
+{
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) { const int u = __shfl_up(v, d, G); if (gl >= d) v += u; }
+    return v;
+}
+template <int G> DEV int grp_incl_min(int v, int gl)
+{
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) { const int u = __shfl_up(v, d, G); if (gl >= d) v = v < u ? v : u; }
+    return v;
+}
+template <int G> DEV int grp_max_all(int v)
+{
+#pragma unroll
+    for (int off = G >> 1; off > 0; off >>= 1) { const int u = __shfl_xor(v, off, G); v = v > u ? v : u; }
+    return v;
+}
+
+// The exact form of diagonal_wins (dev_common.h) for the diagonals it cannot decide: with diagonal score S,
+// every path through ksw_global2's n x n matrix other than the diagonal has either
+//   * g >= 2 insertions and as many deletions: at most (n-2)*mat_max - (o_ins + o_del + 2*(e_ins + e_del)), or
+//   * one insertion and one deletion: it leaves the diagonal at a, runs along diagonal +1 (insertion first:
+//     cells (i, i+1)) or -1 (deletion first: cells (i+1, i)) for i in [a, b), and rejoins at b+1, skipping
+//     diagonal cells a..b: S - oe_ins - oe_del - s0[b] + C[b] - C[a], C the prefix sums of
+//     delta[i] = (shifted cell's score) - s0[i]; the best such path is
+//     S - oe_ins - oe_del + max_b (C[b] - min_{a<=b} C[a] - s0[b]), computed exactly here with scans.
+// When S beats both, the diagonal is the unique optimum and (as in diagonal_wins) the DP's answer is "nM" / S.
+// G lanes cooperate (gl = lane in the group); tq(j, t, q) gives the target and query bases at j.
+template <int G, class TQ>
+DEV bool detour_free(const DOpts &o, const Score sc, int n, int S, TQ tq, int gl)
+{
+    const int64_t bound2 = (int64_t)(n - 2) * o.mat_max - (o.o_ins + o.o_del + 2 * (o.e_ins + o.e_del));
+    if ((int64_t)S <= bound2) return false;
+    const int NEG = -0x3fffffff;
+    int c1 = 0, cm = 0, m1 = 0, mm = 0, x = NEG;   // prefix sums and minima carried across chunks
+    for (int c0 = 0; c0 < n; c0 += G) {
+        const int j = c0 + gl;
+        const bool act = j < n, nx = j + 1 < n;
+        int tj = 0, qj = 0, tn = 0, qn = 0;
+        if (act) tq(j, tj, qj);
+        if (nx) tq(j + 1, tn, qn);
+        const int s0 = act ? sc(tj, qj) : 0;
+        const int d1 = nx ? sc(tj, qn) - s0 : 0, dm = nx ? sc(tn, qj) - s0 : 0;
+        const int i1 = grp_incl_sum<G>(d1, gl), im = grp_incl_sum<G>(dm, gl);
+        const int C1 = c1 + i1 - d1, Cm = cm + im - dm;   // C[j] = sum of delta[i], i < j
+        int n1 = grp_incl_min<G>(act ? C1 : 0x3fffffff, gl), nm = grp_incl_min<G>(act ? Cm : 0x3fffffff, gl);
+        n1 = n1 < m1 ? n1 : m1;
+        nm = nm < mm ? nm : mm;
+        if (act) {
+            const int a1 = C1 - n1 - s0, am = Cm - nm - s0;
+            x = x > a1 ? x : a1;
+            x = x > am ? x : am;
+        }
+        c1 += __shfl(i1, G - 1, G);
+        cm += __shfl(im, G - 1, G);
+        m1 = __shfl(n1, G - 1, G);
+        mm = __shfl(nm, G - 1, G);
+    }
+    x = grp_max_all<G>(x);
+    return (int64_t)x < (int64_t)(o.o_ins + o.e_ins + o.o_del + o.e_del);
+}
+
 // ksw_global2 over accessor-defined sequences.  eh: LDS, qlen+1 entries.  z: LDS (n_col*tlen bytes)
 // or nullptr (score only).  CIGAR (traceback) written to cig[] with libbwa push_cigar semantics.
 extern __shared__ uint8_t g_lds_dp[];   // dynamic LDS of k_reg2aln_w
@@ -297,7 +361,11 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
         for (int i = lane_id(); i < l_query; i += 64) s += sc(ta(i), qa(i));
         s = wave_sum(s);
     }
-    if (l_query == rlen && (w_ == 0 || diagonal_wins(o, l_query, s))) {
+    const bool diag = l_query == rlen &&
+                      (w_ == 0 || diagonal_wins(o, l_query, s) ||
+                       detour_free<64>(o, score_of(o), l_query, s, [&](int j, int &t, int &q) { t = ta(j); q = qa(j); },
+                                       lane_id()));
+    if (diag) {
         if (cap < 1) { ovf = true; return 0; }
         cig[0] = (uint32_t)l_query << 4;
         *ncig = 1;
@@ -577,7 +645,11 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
         for (int i = gl; i < l_query; i += G)
             sum += sc(ref_at(ix, t_start + (int64_t)t_dir * i), g_lds_dp[q_off + q_start + q_dir * i]);
         sum = grp_sum<G>(sum);
-        if (w_ == 0 || diagonal_wins(o, l_query, sum)) {
+        if (w_ == 0 || diagonal_wins(o, l_query, sum) ||
+            detour_free<G>(o, sc, l_query, sum, [&](int j, int &t, int &q) {
+                t = ref_at(ix, t_start + (int64_t)t_dir * j);
+                q = g_lds_dp[q_off + q_start + q_dir * j];
+            }, gl)) {
             if (cap < 1) { ovf = true; return 0; }
             bases += (uint64_t)((rlen + 3) >> 2);
             cig[0] = (uint32_t)l_query << 4;

@@ -272,18 +272,38 @@ def test_ksw_global2_vs_full_matrix():
         assert cigar_score(list(cig)[:n.value], q, t, od, ed, oi_, ei) == sc
 
 
+def _detour_free(t, q, od, ed, oi_, ei):
+    """dp_wave.hip detour_free: S beats every path with >= 2 insertions (bound) and, exactly, every path with one
+    insertion and one deletion (a detour along diagonal +1 or -1)."""
+    n = len(t)
+    s0 = [MAT[t[k] * 5 + q[k]] for k in range(n)]
+    S = sum(s0)
+    if S <= (n - 2) * max(MAT) - (oi_ + od + 2 * (ei + ed)):
+        return False
+    x = -10 ** 9
+    for shift in (1, -1):
+        c = mn = 0
+        for b in range(n):
+            mn = min(mn, c)
+            x = max(x, c - mn - s0[b])
+            if b + 1 < n:
+                c += (MAT[t[b] * 5 + q[b + 1]] if shift == 1 else MAT[t[b + 1] * 5 + q[b]]) - s0[b]
+    return x < oi_ + ei + od + ed
+
+
 def test_diagonal_shortcut_theorem():
-    """dev_common.h diagonal_wins(): for an n x n ksw_global2 whose gapless diagonal scores above
-    (n-1)*mat_max - oe_ins - oe_del, the DP (oracle, full traceback) returns exactly "nM" with the
-    diagonal's score, for every band.  The reg2aln kernels skip the DP on that predicate."""
+    """dev_common.h diagonal_wins() and dp_wave.hip detour_free(): for an n x n ksw_global2 whose gapless diagonal
+    scores S above (n-1)*mat_max - oe_ins - oe_del, or above every detour (exact for one insertion + one
+    deletion, bounded for more), the DP (oracle, full traceback) returns exactly "nM" with score S, for every
+    band.  The reg2aln kernels skip the DP on those predicates."""
     rng = random.Random(12)
     mat_max = max(MAT)
-    hits = 0
-    for trial in range(3000):
+    hits = [0, 0]
+    for trial in range(4000):
         n = rng.choice([1, 2, 3, 5, 8, 20, 60, 150])
         t = [rng.randrange(4) for _ in range(n)]
         q = list(t)
-        for _ in range(rng.choice([0, 1, 1, 2, 2, 3, 4])):
+        for _ in range(rng.choice([0, 1, 1, 2, 2, 3, 4, 5, 6])):
             k = rng.randrange(n)
             q[k] = rng.randrange(5) if rng.random() < 0.2 else (q[k] + rng.randint(1, 3)) % 4
         if rng.random() < 0.3 and n > 8:   # low-complexity stretches: off-diagonal paths score well
@@ -292,16 +312,19 @@ def test_diagonal_shortcut_theorem():
                 t[k] = q[k] = t[s]
         od, ed, oi_, ei = rng.choice([(6, 6, 1, 1), (6, 1, 6, 1), (3, 2, 4, 1), (0, 1, 0, 1), (1, 0, 0, 1)])
         diag = sum(MAT[t[i] * 5 + q[i]] for i in range(n))
-        if diag <= (n - 1) * mat_max - (oi_ + ei) - (od + ed):
+        simple = diag > (n - 1) * mat_max - (oi_ + ei) - (od + ed)
+        exact = _detour_free(t, q, od, ed, oi_, ei)
+        assert exact or not simple, trial   # the exact form decides everything the simple bound does
+        if not exact:
             continue
-        hits += 1
+        hits[simple] += 1
         for w in (0, 1, 3, 8, 100):
             nc = ctypes.c_int()
             cig = (ctypes.c_uint32 * 512)()
             sc = O.lib().orc_ksw_global2(n, bytes(q), n, bytes(t), MAT, od, ed, oi_, ei, w, ctypes.byref(nc), cig, 512)
             assert sc == diag, (trial, w)
             assert list(cig)[:nc.value] == [n << 4], (trial, w, list(cig)[:nc.value])
-    assert hits > 1000
+    assert hits[1] > 1000 and hits[0] > 150   # both the simple bound and the detour scan carry weight
 
 
 # ------------------------------------------------------------------------------- planted reads (KAT)
