@@ -327,9 +327,27 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, const uint8_t *q, int x, int 
     if (q[x] > 3) return x + 1;
     const int c0 = q[x];
     X ik0 = fm.L2(c0) + 1, ik2 = fm.L2(c0 + 1) - fm.L2(c0), ik1 = fm.L2(3 - c0) + 1;
-    int qi = x + 1 < len ? q[x + 1] : 0;
     uint32_t fcode = (uint32_t)c0;
-    for (int i = x + 1; i < len; ++i) {
+    int i0 = x + 1;
+    if (fm.K > 1 && min_len >= fm.K) {
+        // No string of at most K bases can be returned (that needs i - x >= min_len), so the steps through
+        // lengths 2..L (L = min(K, len - x)) only carry the interval forward: one k-mer table read at length L
+        // gives it, unless a hole base ends the walk first (the loop returns just past it).
+        const int L = fm.K < len - x ? fm.K : len - x;
+        int t = 1;
+        for (; t < L; ++t) {
+            const int c = q[x + t];
+            if (c > 3) return x + t + 1;
+            fcode = fcode << 2 | (uint32_t)c;
+        }
+        if (L > 1) {
+            fm.kget(koff(L) + fcode, ik0, ik1, ik2);
+            ++nkm;
+        }
+        i0 = x + L;
+    }
+    int qi = i0 < len ? q[i0] : 0;
+    for (int i = i0; i < len; ++i) {
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;
         if (cur < 4) {
