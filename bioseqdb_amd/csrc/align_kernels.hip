@@ -688,10 +688,10 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
     int hi = EH::kRing ? (qlen < EXT_LDS_COLS - 1 ? qlen : EXT_LDS_COLS - 1) : qlen;   // columns <= hi hold their values
     for (j = 0; j <= hi; ++j) eh.set(j, make_int2(init_h(j), 0));
     max = o.mat_max > 0 ? o.mat_max : 0;
-    max_ins = (int)((double)(qlen * max + end_bonus - o_ins) / e_ins + 1.);
+    max_ins = idiv_plus(qlen * max + end_bonus - o_ins, e_ins, 1);
     max_ins = max_ins > 1 ? max_ins : 1;
     w = w < max_ins ? w : max_ins;
-    max_del = (int)((double)(qlen * max + end_bonus - o_del) / e_del + 1.);
+    max_del = idiv_plus(qlen * max + end_bonus - o_del, e_del, 1);
     max_del = max_del > 1 ? max_del : 1;
     w = w < max_del ? w : max_del;
     max = h0, max_i = max_j = -1; max_ie = -1, gscore = -1;
@@ -881,8 +881,8 @@ DEV int gen_cigar2(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, i
         *score = s;
     } else {
         int w, max_gap, max_ins, max_del, min_w;
-        max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
-        max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+        max_ins = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+        max_del = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
         max_gap = max_ins > max_del ? max_ins : max_del;
         max_gap = max_gap > 1 ? max_gap : 1;
         int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
@@ -1059,8 +1059,8 @@ hipError_t launch_flt_seeds(int grid, hipStream_t st, const DIndex &ix, const DO
 // ------------------------------------------------------------------------------------------------
 DEV int cal_max_gap(const DOpts &o, int qlen)
 {
-    int l_del = (int)((double)(qlen * o.a - o.o_del) / o.e_del + 1.);
-    int l_ins = (int)((double)(qlen * o.a - o.o_ins) / o.e_ins + 1.);
+    int l_del = idiv_plus(qlen * o.a - o.o_del, o.e_del, 1);
+    int l_ins = idiv_plus(qlen * o.a - o.o_ins, o.e_ins, 1);
     int l = l_del > l_ins ? l_del : l_ins;
     l = l > 1 ? l : 1;
     return l < o.w << 1 ? l : o.w << 1;

@@ -92,11 +92,16 @@ DEV int mat_sc(const DOpts &o, int t, int q)
     return (t == 4 || q == 4) ? o.mat_amb : (t == q ? o.mat_match : o.mat_mismatch);
 }
 
+// (int)((double)x / d + k) -- libbwa's band and gap-length formulas -- in integers (d > 0, |x| < 2^31): the
+// double quotient is within an ulp of x/d, which lies at least 1/d from the next integer unless it is one, and
+// both the conversion and C's integer division truncate toward zero, so the two agree for every input
+DEV int idiv_plus(int x, int d, int k) { return (x + k * d) / d; }
+
 DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
 {
     int w;
     if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
-    w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
+    w = idiv_plus((l1 < l2 ? l1 : l2) * a - score - q, r, 2);
     int d = l1 - l2; d = d < 0 ? -d : d;
     if (w < d) w = d;
     return w;

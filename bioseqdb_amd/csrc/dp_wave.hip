@@ -371,8 +371,8 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
         *ncig = 1;
         *score = s;
     } else {
-        int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
-        int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+        int max_ins = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+        int max_del = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
         int max_gap = max_ins > max_del ? max_ins : max_del;
         max_gap = max_gap > 1 ? max_gap : 1;
         int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
@@ -450,8 +450,8 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
                 {   // traceback matrix in LDS when it fits, else in the wave's global slab
                     const int lq = qe - qb;
                     int64_t rl = re - rb;
-                    int mg = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
-                    int md = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+                    int mg = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+                    int md = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
                     mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
                     int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
                     int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
@@ -658,8 +658,8 @@ DEV int gen_cigar2_g(const DIndex &ix, const DOpts &o, int w_, int q_off, int t_
             return 1;
         }
     }
-    int max_ins = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
-    int max_del = (int)((double)(((l_query + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+    int max_ins = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+    int max_del = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
     int max_gap = max_ins > max_del ? max_ins : max_del;
     max_gap = max_gap > 1 ? max_gap : 1;
     int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
@@ -813,8 +813,8 @@ __global__ void k_r2a_key(DOpts o, Caps cp, const int64_t *__restrict__ offs, in
             uint32_t c;
             if (lq == rl && w2 == 0) c = 0;
             else {
-                int mg = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_ins) / o.e_ins + 1.);
-                int md = (int)((double)(((lq + 1) >> 1) * o.mat_match - o.o_del) / o.e_del + 1.);
+                int mg = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+                int md = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
                 mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
                 int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
                 int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;

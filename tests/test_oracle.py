@@ -416,3 +416,15 @@ def test_ksw_align2_score_identity_and_bounds():
         # without insertions (a prohibitive open penalty) F never fires: the striped result is the optimum
         assert _ksw(q, t, mat, oi=1000) == _gotoh_local(q, t, list(mat), 6, 6, 1000, 1)
 
+
+
+def test_integer_band_formulas_equal_double():
+    """dev_common.h idiv_plus: (x + k*d) / d in C integers equals libbwa's (int)((double)x / d + k) for the
+    band / gap-length formulas (cal_max_gap, ksw_extend2's max_ins/max_del, bwa_gen_cigar2, infer_bw)."""
+    def c_div(a, d):   # C: truncation toward zero
+        q = abs(a) // d
+        return q if a >= 0 else -q
+    for d in range(1, 70):
+        for k in (1, 2):
+            for x in list(range(-3000, 3001)) + [2 ** 30 - 7, -(2 ** 30) + 5]:
+                assert c_div(x + k * d, d) == int(x / d + k), (x, d, k)
