@@ -1081,7 +1081,7 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
         HIPCHK(launch_ext_key(st, w.cp, (b->offs + b->lo), sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
         size_t tb = w.esort_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 16, st));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 24, st));
         order = w.eidx1;
     }
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,
