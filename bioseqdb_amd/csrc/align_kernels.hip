@@ -296,8 +296,10 @@ DEV void ks_combsort(int *a, int n, LT lt)
     if (gap != 1) ks_insertsort(a, n, lt);
 }
 
+// stk: 3 x 64 ints of the thread's global scratch (the partition stack, touched only by partitions of more
+// than 16 elements): a private array here would give every wave of the kernel a scratch segment
 template <class LT>
-DEV void ks_introsort(int *a, int n, LT lt)
+DEV void ks_introsort(int *a, int n, LT lt, int *stk)
 {
     if (n < 1) return;
     if (n == 2) {
@@ -306,7 +308,7 @@ DEV void ks_introsort(int *a, int n, LT lt)
     }
     int d;
     for (d = 2; (1ul << d) < (unsigned long)n; ++d);
-    int stk_l[64], stk_r[64], stk_d[64], top = 0;
+    int *stk_l = stk, *stk_r = stk + 64, *stk_d = stk + 128, top = 0;
     int s = 0, t = n - 1;
     d <<= 1;
     while (1) {
@@ -508,6 +510,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
     C.cap_nodes = cp.chains / 2 + 8;
     int *ord = reinterpret_cast<int *>(reinterpret_cast<uint8_t *>(C.nodes) + (size_t)C.cap_nodes * sizeof(KNode));
     int *kept_list = ord + cp.chains;
+    int *stk = kept_list + cp.chains;      // introsort stack (192 ints), then the B-tree walk's (3 x 24)
     for (int li = tid; li < n; li += nthr) {
         n_chains[li] = 0;
         if (status[li]) continue;
@@ -552,7 +555,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         // in-order traversal of the B-tree -> chain order
         int nord = 0;
         {   // iterative in-order walk == kbtree's __kb_traverse
-            int stn[24], sti[24], std_[24], sp = 0;
+            int *stn = stk + 192, *sti = stn + 24, *std_ = sti + 24, sp = 0;
             stn[0] = C.root; sti[0] = 0; std_[0] = 0;
             while (sp >= 0) {
                 const KNode &nd = C.nodes[stn[sp]];
@@ -577,7 +580,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         }
         if (n_chn > 0) {
             ChainNode *ch = C.ch;
-            ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; });
+            ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; }, stk);
             ch[ord[0]].kept = 3;
             int nk = 0;
             kept_list[nk++] = 0;
@@ -857,6 +860,77 @@ DEVN int ksw_global2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
     return score;
 }
 
+// ksw_global2's score alone, inlined (mem_patch_reg's use in the extension stage): the same recurrences as
+// ksw_global2 above without the traceback, so the extension kernel makes no out-of-line call and needs no
+// private stack segment.
+DEV int ksw_global2_score(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
+                          int e_ins, int w, int2 *eh, uint64_t &cells)
+{
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    const Score sc = score_of(o);
+    eh[0] = make_int2(0, MINUS_INF);
+    int j;
+    for (j = 1; j <= qlen && j <= w; ++j) eh[j] = make_int2(-(o_ins + e_ins * j), MINUS_INF);
+    for (; j <= qlen; ++j) eh[j] = make_int2(MINUS_INF, MINUS_INF);
+    for (int i = 0; i < tlen; ++i) {
+        int32_t f = MINUS_INF, h1, t;
+        const int tb = target(i);
+        const int beg = i > w ? i - w : 0;
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        h1 = beg == 0 ? -(o_del + e_del * (i + 1)) : MINUS_INF;
+        cells += (uint64_t)(end > beg ? end - beg : 0);
+        for (j = beg; j < end; ++j) {
+            int2 p = eh[j];
+            int32_t h, m = p.x, e = p.y;
+            p.x = h1;
+            m += sc(tb, query(j));
+            h = m >= e ? m : e;
+            h = h >= f ? h : f;
+            h1 = h;
+            t = m - oe_del;
+            e -= e_del;
+            e = e > t ? e : t;
+            p.y = e;
+            eh[j] = p;
+            t = m - oe_ins;
+            f -= e_ins;
+            f = f > t ? f : t;
+        }
+        eh[end] = make_int2(h1, MINUS_INF);
+    }
+    return eh[qlen].x;
+}
+
+// bwa_gen_cigar2's score for mem_patch_reg (no CIGAR)
+DEV int gen_cigar2_score(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
+                         int64_t re, int *score, int2 *eh, uint64_t &cells, uint64_t &bases)
+{
+    if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
+    const int64_t rlen = re - rb;
+    if (re > (ix.l_pac << 1) || rb < 0) return 0;
+    bases += (uint64_t)((rlen + 3) >> 2);
+    const bool rev = rb >= ix.l_pac;
+    QAcc qa{q, rev ? qb + l_query - 1 : qb, rev ? -1 : 1};
+    TAcc ta{&ix, rev ? re - 1 : rb, rev ? -1 : 1};
+    if (l_query == rlen && w_ == 0) {
+        int s = 0;
+        for (int i = 0; i < l_query; ++i) s += mat_sc(o, ta(i), qa(i));
+        *score = s;
+        return 1;
+    }
+    int max_ins = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+    int max_del = idiv_plus(((l_query + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
+    int max_gap = max_ins > max_del ? max_ins : max_del;
+    max_gap = max_gap > 1 ? max_gap : 1;
+    int dl = (int)rlen - l_query; dl = dl < 0 ? -dl : dl;
+    int w = (max_gap + dl + 1) >> 1;
+    w = w < w_ ? w : w_;
+    const int min_w = dl + 3;
+    w = w > min_w ? w : min_w;
+    *score = ksw_global2_score(o, l_query, qa, (int)rlen, ta, o.o_del, o.e_del, o.o_ins, o.e_ins, w, eh, cells);
+    return 1;
+}
+
 // bwa_gen_cigar2 (score + CIGAR; MD/NM are not part of bioseqdb's output)
 DEV int gen_cigar2(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
                    int64_t re, int *score, int2 *eh, uint8_t *z, int64_t zcap, uint32_t *cig, int cap, int *ncig,
@@ -1085,6 +1159,7 @@ struct ExtCtx {
     int *idx;
     uint64_t *srt;
     int2 *eh;
+    int *stk;   // introsort stack (192 ints)
     bool ovf;
 };
 
@@ -1268,9 +1343,7 @@ DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg 
     } else if (w > o.w << 2 || r >= 0.05f * 2) return 0;
     w += a.w + b.w;
     w = w < o.w << 2 ? w : o.w << 2;
-    int ncig = 0;
-    bool dummy = false;
-    gen_cigar2(ix, o, w, q, a.qb, b.qe - a.qb, a.rb, b.re, &score, eh, nullptr, 0, nullptr, 0, &ncig, dummy, cells, bases);
+    gen_cigar2_score(ix, o, w, q, a.qb, b.qe - a.qb, a.rb, b.re, &score, eh, cells, bases);
     q_s = (int)((double)(b.qe - a.qb) / ((b.qe - b.qb) + (a.qe - a.qb)) * (b.score + a.score) + .499);
     r_s = (int)((double)(b.re - a.rb) / ((b.re - b.rb) + (a.re - a.rb)) * (b.score + a.score) + .499);
     if ((double)score / (q_s > r_s ? q_s : r_s) < 0.90f) return 0;
@@ -1293,7 +1366,7 @@ DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, Ext
     if (n <= 1) return n;
     Reg *a = X.av;
     for (i = 0; i < n; ++i) X.idx[i] = i;
-    ks_introsort(X.idx, n, [a](int x, int y) { return a[x].re < a[y].re; });
+    ks_introsort(X.idx, n, [a](int x, int y) { return a[x].re < a[y].re; }, X.stk);
     permute(X, n);
     for (i = 0; i < n; ++i) a[i].n_comp = 1;
     for (i = 1; i < n; ++i) {
@@ -1329,7 +1402,7 @@ DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, Ext
     for (i = 0; i < n; ++i) X.idx[i] = i;
     ks_introsort(X.idx, n, [a](int x, int y) {
         return a[x].score > a[y].score || (a[x].score == a[y].score && (a[x].rb < a[y].rb || (a[x].rb == a[y].rb && a[x].qb < a[y].qb)));
-    });
+    }, X.stk);
     permute(X, n);
     for (i = 1; i < n; ++i)
         if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
@@ -1349,7 +1422,7 @@ DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
     }
     ks_introsort(X.idx, n, [a](int x, int y) {
         return a[x].score > a[y].score || (a[x].score == a[y].score && a[x].hash < a[y].hash);
-    });
+    }, X.stk);
     permute(X, n);
     int tmp = o.a + o.b;
     tmp = o.o_del + o.e_del > tmp ? o.o_del + o.e_del : tmp;
@@ -1393,6 +1466,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
     X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
     X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
+    X.stk = reinterpret_cast<int *>(X.eh + cp.max_len + 2);
     for (int it = tid; it < n; it += nthr) {
         const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;

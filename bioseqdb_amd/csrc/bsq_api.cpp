@@ -703,9 +703,11 @@ bool long_reads(int max_len)
 int64_t scratch_bytes(const Caps &c, int64_t z_cap)
 {
     int64_t smem = 3LL * (c.max_len + 2) * (int64_t)sizeof(Intv);
-    int64_t chain = (int64_t)c.seeds * 24 + (int64_t)c.chains * 40 + (int64_t)(c.chains / 2 + 8) * 84 + 2LL * c.chains * 4;
+    // + the sort / tree-walk stacks kept in this scratch instead of private memory (align_kernels.hip)
+    int64_t chain = (int64_t)c.seeds * 24 + (int64_t)c.chains * 40 + (int64_t)(c.chains / 2 + 8) * 84 + 2LL * c.chains * 4 +
+                    (192 + 72) * 4;
     int64_t ext = (int64_t)c.regs * (int64_t)sizeof(Reg) + ((c.regs * 4 + 15) & ~15) + (int64_t)c.seeds * 8 +
-                  (int64_t)(c.max_len + 2) * 8;
+                  (int64_t)(c.max_len + 2) * 8 + 192 * 4;
     int64_t r2a = (((int64_t)(c.max_len + 2) * 8 + 63) & ~63LL) + z_cap;
     int64_t m = std::max(std::max(smem, chain), std::max(ext, r2a));
     return (m + 255) & ~255LL;
