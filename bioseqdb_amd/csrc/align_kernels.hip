@@ -557,6 +557,11 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         {   // iterative in-order walk == kbtree's __kb_traverse
             int *stn = stk + 192, *sti = stn + 24, *std_ = sti + 24, sp = 0;
             stn[0] = C.root; sti[0] = 0; std_[0] = 0;
+            if (!C.nodes[C.root].is_internal) {   // a lone leaf root (<= 9 chains, the common case): its keys
+                const KNode &nd = C.nodes[C.root];
+                for (int i = 0; i < nd.n; ++i) ord[nord++] = nd.key[i];
+                sp = -1;
+            }
             while (sp >= 0) {
                 const KNode &nd = C.nodes[stn[sp]];
                 const int i = sti[sp];
