@@ -755,7 +755,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.eidx0, R * 4));
         HIPCHK(hipMalloc(&w.eidx1, R * 4));
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, w.esort_bytes, w.ekey0, w.ekey1, w.eidx0, w.eidx1, (int)R,
-                                                  0, 16));
+                                                  0, 24));   // the widest key sorted (the extension's, 24 bits)
         HIPCHK(hipMalloc(&w.esort_tmp, std::max<size_t>(w.esort_bytes, 16)));
     }
     return BSQ_OK;
@@ -981,7 +981,10 @@ static int prepare_workspace(bsq_batch *b, int max_len)
     if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1) || want != b->chunk) {
         b->main.release();
         b->chunk = want;
-        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device), 32 * 1024, false);
+        // per-thread scratch: the main pass's reg2aln keeps its traceback in LDS and the zslab unless reads are
+        // longer than 1024 bases (then the serial kernel's 32 KB traceback area is needed)
+        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device),
+                          max_len > 1024 ? 32 * 1024 : 0, false);
         if (rc) return rc;
     }
     return BSQ_OK;
