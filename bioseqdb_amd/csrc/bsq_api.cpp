@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <queue>
 #include <string>
 #include <thread>
 #include <vector>
@@ -60,7 +61,7 @@ hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
 struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
 struct RenderView {
     const bsq_hit *hits; const uint32_t *cigar; int64_t n_hits; const uint8_t *pac; int64_t l_pac;
-    const RenderHole *holes; int32_t n_holes; int64_t hole_max; const uint8_t *codes; const int64_t *offs;
+    const RenderHole *holes; int64_t n_holes; const uint8_t *codes; const int64_t *offs;
     const int64_t *rh_off; const RenderHole *rh;
 };
 hipError_t launch_row_len(hipStream_t, const RenderView &, int64_t *);
@@ -1622,14 +1623,9 @@ static int render_inputs(bsq_batch *b, const void *const *reads, RenderInputs &r
     { int rc = grow_dev(b->r_len, b->r_len_cap, H.n_hits + 1); if (rc) return rc; }
     HIPCHK(hipMemcpyAsync(b->r_hits, H.hits, (size_t)H.n_hits * sizeof(bsq_hit), hipMemcpyHostToDevice, st));
     if (H.n_cigar) HIPCHK(hipMemcpyAsync(b->r_cig, H.cigar, (size_t)H.n_cigar * 4, hipMemcpyHostToDevice, st));
-    // reference holes by offset (the order field keeps the reference's overwrite order, Q3)
+    // the reference's hole overlay as disjoint segments (bsq_index.h HoleIndex, shared with the host renderer)
     std::vector<RenderHole> rh;
-    int64_t hole_max = 0;
-    for (size_t i = 0; i < h.holes.size(); ++i) {
-        rh.push_back(RenderHole{h.holes[i].offset, h.holes[i].offset + h.holes[i].len, (uint32_t)i, (uint8_t)h.holes[i].amb});
-        hole_max = std::max<int64_t>(hole_max, h.holes[i].len);
-    }
-    std::sort(rh.begin(), rh.end(), [](const RenderHole &a, const RenderHole &c) { return a.beg < c.beg; });
+    for (const HoleRef &x : b->idx->holes().segs) rh.push_back(RenderHole{x.beg, x.end, x.order, (uint8_t)x.amb});
     // the reads' own hole symbols (nuclseq varlenas); without them, ambiguous bases print as N
     std::vector<int64_t> qoff;
     std::vector<RenderHole> qh;
@@ -1659,7 +1655,7 @@ static int render_inputs(bsq_batch *b, const void *const *reads, RenderInputs &r
         HIPCHK(hipMemcpyAsync(d_qh, qh.data(), qh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(d_qoff, qoff.data(), qoff.size() * 8, hipMemcpyHostToDevice, st));
     }
-    ri.v = RenderView{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int32_t)rh.size(), hole_max, b->codes,
+    ri.v = RenderView{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int64_t)rh.size(), b->codes,
                       b->offs, d_qoff, d_qh};
     return BSQ_OK;
 }

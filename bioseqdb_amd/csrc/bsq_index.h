@@ -47,20 +47,20 @@ struct DeviceIndex;   // bsq_api.cpp
 
 struct HoleRef { int64_t beg, end; uint32_t order; char amb; };
 
-// Holes ordered by offset, with the longest length: the holes overlapping [rb, re) are those with offset
-// in (rb - max_len, re).  Overlapping holes (Q3: offsets of different rows share one axis) are applied
-// in their original order, as extract_reference_subseq's loop does (bioseqdb/bwa.cpp:61-66).
+// The reference's hole overlay as disjoint, offset-ordered segments.  extract_reference_subseq writes the
+// holes in their original order (bioseqdb/bwa.cpp:61-66), and holes of different rows share one axis
+// (Q3), so they can overlap: the symbol left at p is that of the highest-order hole covering p.  Built
+// once per index by a sweep over hole starts/ends with a max-heap on the order (expired holes dropped
+// lazily); a window [rb, re) then costs one binary search plus the segments it overlaps, however many
+// long holes lie under it.  `order` is the winning hole's index.
 struct HoleIndex {
-    std::vector<HoleRef> by_off;
-    int64_t max_len = 0;
-    explicit HoleIndex(const std::vector<Hole> &holes)
+    std::vector<HoleRef> segs;
+    explicit HoleIndex(const std::vector<Hole> &holes);
+    // first segment with end > rb (segments are disjoint, so ends increase with begs)
+    size_t first_after(int64_t rb) const
     {
-        by_off.reserve(holes.size());
-        for (size_t i = 0; i < holes.size(); ++i) {
-            by_off.push_back(HoleRef{holes[i].offset, holes[i].offset + holes[i].len, (uint32_t)i, holes[i].amb});
-            max_len = std::max<int64_t>(max_len, holes[i].len);
-        }
-        std::sort(by_off.begin(), by_off.end(), [](const HoleRef &a, const HoleRef &b) { return a.beg < b.beg; });
+        return (size_t)(std::upper_bound(segs.begin(), segs.end(), rb,
+                                         [](int64_t v, const HoleRef &a) { return v < a.end; }) - segs.begin());
     }
 };
 

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <queue>
 #include <string>
 #include <thread>
 #include <vector>
@@ -17,6 +18,32 @@
 #include "bsq_index.h"
 
 using namespace bsq;
+
+bsq::HoleIndex::HoleIndex(const std::vector<Hole> &holes)
+{
+    std::vector<uint32_t> by_beg;
+    std::vector<int64_t> cuts;   // every start and end, sorted, distinct
+    for (size_t i = 0; i < holes.size(); ++i)
+        if (holes[i].len > 0) {
+            by_beg.push_back((uint32_t)i);
+            cuts.push_back(holes[i].offset);
+            cuts.push_back(holes[i].offset + holes[i].len);
+        }
+    std::sort(by_beg.begin(), by_beg.end(), [&](uint32_t a, uint32_t b) { return holes[a].offset < holes[b].offset; });
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    std::priority_queue<uint32_t> live;   // hole indices = overwrite order
+    size_t si = 0;
+    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
+        const int64_t a = cuts[c], b = cuts[c + 1];
+        while (si < by_beg.size() && holes[by_beg[si]].offset <= a) live.push(by_beg[si++]);
+        while (!live.empty() && holes[live.top()].offset + holes[live.top()].len <= a) live.pop();
+        if (live.empty()) continue;
+        const uint32_t w = live.top();
+        if (!segs.empty() && segs.back().end == a && segs.back().amb == holes[w].amb) segs.back().end = b;
+        else segs.push_back(HoleRef{a, b, w, holes[w].amb});
+    }
+}
 
 namespace {
 
@@ -27,24 +54,9 @@ void ref_subseq(const HostIndex &h, const HoleIndex &hx, int64_t rb, int64_t re,
     char *s = &out[base];
     if (rb < h.l_pac) {
         for (int64_t i = 0; i < re - rb; ++i) s[i] = "ACGT"[pac_get(h.pac.data(), (uint64_t)(rb + i))];
-        if (hx.by_off.empty()) return;
-        const int64_t lo_off = rb - hx.max_len;
-        auto it = std::lower_bound(hx.by_off.begin(), hx.by_off.end(), lo_off,
-                                   [](const HoleRef &a, int64_t v) { return a.beg < v; });
-        HoleRef hit[64];
-        int nh = 0;
-        std::vector<HoleRef> many;
-        for (; it != hx.by_off.end() && it->beg < re; ++it) {
-            if (it->end <= rb) continue;
-            if (nh < 64) hit[nh++] = *it; else many.push_back(*it);
-        }
-        if (!many.empty()) many.insert(many.begin(), hit, hit + nh);
-        HoleRef *v = many.empty() ? hit : many.data();
-        const size_t n = many.empty() ? (size_t)nh : many.size();
-        std::sort(v, v + n, [](const HoleRef &a, const HoleRef &b) { return a.order < b.order; });
-        for (size_t k = 0; k < n; ++k) {
-            const int64_t lo = std::max<int64_t>(v[k].beg, rb), hi = std::min<int64_t>(v[k].end, re);
-            for (int64_t i = lo; i < hi; ++i) s[i - rb] = v[k].amb;
+        for (size_t k = hx.first_after(rb); k < hx.segs.size() && hx.segs[k].beg < re; ++k) {
+            const int64_t lo = std::max<int64_t>(hx.segs[k].beg, rb), hi = std::min<int64_t>(hx.segs[k].end, re);
+            for (int64_t i = lo; i < hi; ++i) s[i - rb] = hx.segs[k].amb;
         }
     } else {
         // Q7: the reference reads past the forward pac here (undefined behaviour); render the

@@ -25,9 +25,8 @@ struct RenderView {
     int64_t n_hits;
     const uint8_t *pac;
     int64_t l_pac;
-    const RenderHole *holes;   // reference holes ordered by offset
-    int32_t n_holes;
-    int64_t hole_max;          // longest reference hole
+    const RenderHole *holes;   // the reference's hole overlay: disjoint segments ordered by offset
+    int64_t n_holes;
     const uint8_t *codes;      // read codes (nt4) of the batch, read r at offs[r]
     const int64_t *offs;
     const int64_t *rh_off;     // read r's holes: [rh_off[r], rh_off[r+1]) of rh (nullptr: none)
@@ -77,25 +76,13 @@ DEV char *ref_subseq(const RenderView &v, const bsq_hit &x, char *o)
     const int64_t rb = x.rb, re = x.re;
     if (rb < v.l_pac) {
         for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[pac_base(v.pac, i)];
-        if (v.n_holes) {   // holes with beg in (rb - hole_max, re), applied in their original order
-            int lo = 0, hi = v.n_holes;
-            const int64_t from = rb - v.hole_max;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (v.holes[mid].beg < from) lo = mid + 1; else hi = mid; }
-            uint32_t done = 0;   // apply by increasing order: repeatedly the smallest order above `done`
-            for (;;) {
-                uint32_t best = 0xffffffffu;
-                int bi = -1;
-                for (int h = lo; h < v.n_holes && v.holes[h].beg < re; ++h) {
-                    const RenderHole &H = v.holes[h];
-                    if (H.end <= rb || H.order + 1 <= done) continue;
-                    if (H.order < best) { best = H.order; bi = h; }
-                }
-                if (bi < 0) break;
-                const RenderHole &H = v.holes[bi];
-                const int64_t a = H.beg > rb ? H.beg : rb, b = H.end < re ? H.end : re;
-                for (int64_t i = a; i < b; ++i) s[i - rb] = (char)H.amb;
-                done = H.order + 1;
-            }
+        // the hole overlay as disjoint segments (HoleIndex): the first one ending after rb, then in order
+        int64_t lo = 0, hi = v.n_holes;
+        while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (v.holes[mid].end <= rb) lo = mid + 1; else hi = mid; }
+        for (int64_t h = lo; h < v.n_holes && v.holes[h].beg < re; ++h) {
+            const RenderHole &H = v.holes[h];
+            const int64_t a = H.beg > rb ? H.beg : rb, b = H.end < re ? H.end : re;
+            for (int64_t i = a; i < b; ++i) s[i - rb] = (char)H.amb;
         }
     } else {   // Q7: the reverse-strand reference text
         for (int64_t i = rb; i < re; ++i) *o++ = "ACGT"[3 - pac_base(v.pac, (v.l_pac << 1) - 1 - i)];

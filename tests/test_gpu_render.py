@@ -79,3 +79,45 @@ def test_gpu_render_matches_host(monkeypatch, chunk):
                 assert raw[a0:a0 + size] == NucleotideSequence._encode(f[col]).raw, (k, col)
     finally:
         L.bsq_batch_free(b)
+
+
+def test_gpu_render_overlapping_long_holes():
+    """An hg38-like N-gap layout (long gaps in every row pile up on the row-relative axis, Q3): the GPU rows
+    under hundreds of overlapping holes equal the host renderer's (both read the disjoint overlay segments
+    of HoleIndex; tests/test_render.py pins the host against extract_reference_subseq's loop)."""
+    r = random.Random(23)
+    from test_render import _gapped_refs, _decode
+    refs = _gapped_refs(r)
+    texts = [_decode(ns)[0][:40000] for ns in refs]   # row texts without the overlay: reads come from real bases
+    pi, _ = build_pair([ns.to_text() for ns in refs])
+    pi.upload()
+    rtexts = []
+    for k in range(3000):
+        row = texts[0 if k % 3 else r.randrange(len(texts))]
+        p = r.randrange(0, len(row) - 150)
+        rtexts.append(row[p:p + 150])
+    seqs = [NucleotideSequence.from_text(t) for t in rtexts]
+    codes = np.frombuffer("".join(rtexts).encode(), np.uint8)
+    lut = np.full(256, 4, np.uint8)
+    for c, v in zip(b"ACGT", range(4)):
+        lut[c] = v
+    codes = np.ascontiguousarray(lut[codes])
+    offs = np.arange(len(rtexts) + 1, dtype=np.int64) * 150
+    L = N.lib()
+    b = ctypes.c_void_p()
+    N.check(L.bsq_batch_create(pi.handle, len(rtexts), int(offs[-1]), ctypes.byref(b)))
+    try:
+        N.check(L.bsq_batch_set_reads(b, codes.ctypes.data, offs.ctypes.data, len(rtexts)))
+        N.check(L.bsq_batch_run(b, ctypes.byref(pi.options), 0))
+        arr = (ctypes.c_void_p * len(seqs))(*[s.ptr for s in seqs])
+        p = L.bsq_render_tsv(pi.handle, L.bsq_batch_hits(b), arr)
+        host = ctypes.string_at(p)
+        L.bsq_free(p)
+        t, n = ctypes.c_void_p(), ctypes.c_int64()
+        N.check(L.bsq_batch_render(b, arr, ctypes.byref(t), ctypes.byref(n)))
+        gpu = ctypes.string_at(t, n.value)
+        assert host.count(b"\n") >= 2000 and gpu == host
+        under = sum(1 for row in host.decode().splitlines() if set(row.split("\t")[1]) & set("NRYK"))
+        assert under >= 100   # rows whose ref_subseq carries overlay symbols
+    finally:
+        L.bsq_batch_free(b)

@@ -20,12 +20,17 @@ def _decode(ns):
     return text, [(o, l, c.decode()) for o, l, c in holes]
 
 
-def _expected_ref_subseq(seqs, rb, re):
+def _concat(seqs):
     pac, holes = "", []
     for ns in seqs:
         t, h = _decode(ns)
         pac += t
         holes += h   # offsets stay row-relative (Q3)
+    return pac, holes
+
+
+def _expected_ref_subseq(seqs, rb, re, cat=None):
+    pac, holes = cat or _concat(seqs)
     s = list(pac[rb:re])
     for o, l, c in holes:
         for i in range(max(o, rb), min(o + l, re)):
@@ -86,3 +91,46 @@ def test_render_threads_and_hole_overlay(monkeypatch):
         assert row.ref_subseq == _expected_ref_subseq(refs, rec["rb"], rec["re"])
         assert row.cigar == f"{rec['qb']}N{150 - rec['qb']}M"   # clip op 3 prints as 'N' (Q8)
         assert row.score == rec["score"]
+
+
+def _gapped_refs(r, rows=12, n=40000):
+    """An hg38-like N-gap layout: every row has a long centromere-like gap plus telomere and scattered gaps of
+    N and IUPAC symbols, so (Q3) the holes of all rows pile up on the shared row-relative axis."""
+    texts = []
+    for _ in range(rows):
+        t = [r.choice("ACGT") for _ in range(n)]
+        spans = [(0, r.randrange(50, 500)), (r.randrange(n // 3, n // 2), r.randrange(5000, 15000)),
+                 (n - r.randrange(50, 500), n)]
+        spans = [(a, a + b) if b < a else (a, b) for a, b in spans[:2]] + [spans[2]]
+        spans += [(o, o + r.randrange(1, 300)) for o in (r.randrange(0, n - 300) for _ in range(40))]
+        for a, b in spans:
+            t[a:b] = r.choice("NNNRYK") * (min(b, n) - a)
+        texts.append("".join(t[:n]))
+    return [NucleotideSequence.from_text(t) for t in texts]
+
+
+def test_render_overlapping_long_holes(monkeypatch):
+    """Windows under hundreds of overlapping long holes (the overlay is one binary search plus the
+    disjoint segments a window touches) give extract_reference_subseq's text."""
+    r = random.Random(11)
+    refs = _gapped_refs(r)
+    idx = BwaIndex()
+    for i, ns in enumerate(refs):
+        idx.add_ref_sequence(7 + i, ns)
+    idx.build()
+    l_pac = N.lib().bsq_index_l_pac(idx.handle)
+    reads = [NucleotideSequence.from_text("ACGT" * 40)]
+    records, cigars = [], []
+    for k in range(1500):
+        rb = r.randrange(0, 45000) if k % 2 else r.randrange(0, l_pac - 400)
+        re = min(rb + r.randrange(1, 400), l_pac)
+        records.append(dict(ref_id=7, rb=rb, re=re, ref_match_start=rb, ref_match_end=re, ref_match_len=re - rb,
+                            qb=0, qe=160, score=1, rid=0, is_primary=1, is_secondary=0, is_reverse=0, read_index=0,
+                            cigar_off=0, n_cigar=1))
+    cigars = [(160 << 4) | 0]
+    text = _render(idx, reads, records, [0, len(records)], cigars, 4, monkeypatch)
+    rows = B.parse_tsv(text)
+    assert len(rows) == len(records)
+    cat = _concat(refs)
+    for rec, row in zip(records, rows):
+        assert row.ref_subseq == _expected_ref_subseq(refs, rec["rb"], rec["re"], cat)
