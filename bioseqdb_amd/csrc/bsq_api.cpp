@@ -750,7 +750,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
         HIPCHK(hipMalloc(&w.dcount, 16));
-        HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 2)));
+        HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 4)));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
         HIPCHK(hipMalloc(&w.ekey1, R * 4));
         HIPCHK(hipMalloc(&w.eidx0, R * 4));

@@ -184,27 +184,37 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
 // first entry of the k-mer table level for strings of length L: (4^L - 4) / 3
 DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
 
-// The lane's list of (x0, x2, end) entries: entries e < cap in LDS (entry e at base[e * stride],
+// The lane's list of (x0, x2, end) entries: entries e < cap in LDS (entry e at element offset e * stride,
 // lane-interleaved), the next gcap in this read's global spill area (lists longer than the LDS share
-// are rare; they cost global accesses instead of a retry).
+// are rare; they cost global accesses instead of a retry).  The LDS part is addressed by offsets into the
+// dynamic LDS arrays and the spill part is read with (relaxed, wave-scope) atomic loads, so the compiler
+// cannot merge the two branches' loads into one flat load through a selected pointer: flat loads of LDS
+// go through the vector memory pipeline and make every wait cover both counters.
+extern __shared__ uint32_t g_smem_u32[];
+extern __shared__ uint64_t g_smem_u64[];
+extern __shared__ uint16_t g_smem_u16[];
+template <typename X> DEV X &lds_x(int i);
+template <> DEV uint32_t &lds_x<uint32_t>(int i) { return g_smem_u32[i]; }
+template <> DEV uint64_t &lds_x<uint64_t>(int i) { return g_smem_u64[i]; }
+template <typename T> DEV T spill_load(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
+
 template <typename X>
 struct LList {
-    X *x0, *x2;
-    uint16_t *end;
+    int x0, x2, end;   // element offsets of this lane's entry 0: x0/x2 in X units, end in u16 units
     int stride, cap;
     X *gx0, *gx2;
-    uint16_t *gend;
+    uint32_t *gend;
     int gcap;
     DEV int total() const { return cap + gcap; }
     DEV void set(int e, X a, X b, int en)
     {
-        if (e < cap) { x0[e * stride] = a; x2[e * stride] = b; end[e * stride] = (uint16_t)en; }
-        else { const int g = e - cap; gx0[g] = a; gx2[g] = b; gend[g] = (uint16_t)en; }
+        if (e < cap) { lds_x<X>(x0 + e * stride) = a; lds_x<X>(x2 + e * stride) = b; g_smem_u16[end + e * stride] = (uint16_t)en; }
+        else { const int g = e - cap; gx0[g] = a; gx2[g] = b; gend[g] = (uint32_t)en; }
     }
     DEV void get(int e, X &a, X &b, int &en) const
     {
-        if (e < cap) { a = x0[e * stride]; b = x2[e * stride]; en = end[e * stride]; }
-        else { const int g = e - cap; a = gx0[g]; b = gx2[g]; en = gend[g]; }
+        if (e < cap) { a = lds_x<X>(x0 + e * stride); b = lds_x<X>(x2 + e * stride); en = g_smem_u16[end + e * stride]; }
+        else { const int g = e - cap; a = spill_load(gx0 + g); b = spill_load(gx2 + g); en = (int)spill_load(gend + g); }
     }
 };
 
@@ -380,19 +390,18 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap)
 {
-    extern __shared__ uint8_t lds_raw[];
     const int T = blockDim.x, t = threadIdx.x;
     LList<X> L;
-    L.x0 = reinterpret_cast<X *>(lds_raw) + t;
-    L.x2 = reinterpret_cast<X *>(lds_raw) + (size_t)T * lcap + t;
-    L.end = reinterpret_cast<uint16_t *>(lds_raw + (size_t)2 * T * lcap * sizeof(X)) + t;
+    L.x0 = t;
+    L.x2 = T * lcap + t;
+    L.end = (int)((size_t)2 * T * lcap * sizeof(X) / 2) + t;
     L.stride = T;
     L.cap = lcap;
-    {   // spill area: [x0: n*gcap X][x2: n*gcap X][end: n*gcap u16], this read's gcap entries of each
+    {   // spill area: [x0: n*gcap X][x2: n*gcap X][end: n*gcap u32], this read's gcap entries of each
         const size_t me = (size_t)(blockIdx.x * T + t) * (size_t)gcap, tot = (size_t)n * (size_t)gcap;
         L.gx0 = reinterpret_cast<X *>(spill) + me;
         L.gx2 = reinterpret_cast<X *>(spill) + tot + me;
-        L.gend = reinterpret_cast<uint16_t *>(spill + 2 * tot * sizeof(X)) + me;
+        L.gend = reinterpret_cast<uint32_t *>(spill + 2 * tot * sizeof(X)) + me;
         L.gcap = spill ? gcap : 0;
     }
     FM<X> fm;
