@@ -27,17 +27,33 @@ struct FM {
     const OccBlock32 *occ32;   // 64-base blocks, used when X is u32
     const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
     int K;
-    // table entry idx: (x[0], x[1], x[2]) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B)
+    // table entry idx: (x[0], x[2], x[1], 0) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B); (x[0], x[2])
+    // first, so the backward phase (which never reads x[1]) takes one 8-B (16-B) load per entry
     DEV void kget(uint32_t idx, X &a0, X &a1, X &a2) const
     {
         if constexpr (sizeof(X) == 4) {
             const uint4 e = kt[idx];
-            a0 = e.x; a1 = e.y; a2 = e.z;
+            a0 = e.x; a2 = e.y; a1 = e.z;
         } else {
             const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(kt) + 2 * (size_t)idx;
             const ulonglong2 u = p[0], v = p[1];
-            a0 = u.x; a1 = u.y; a2 = v.x;
+            a0 = u.x; a2 = u.y; a1 = v.x;
         }
+    }
+    DEV void kget02(uint32_t idx, X &a0, X &a2) const
+    {
+        if constexpr (sizeof(X) == 4) {
+            const uint2 e = reinterpret_cast<const uint2 *>(kt)[2 * (size_t)idx];
+            a0 = e.x; a2 = e.y;
+        } else {
+            const ulonglong2 u = reinterpret_cast<const ulonglong2 *>(kt)[2 * (size_t)idx];
+            a0 = u.x; a2 = u.y;
+        }
+    }
+    DEV X kget1(uint32_t idx) const
+    {
+        if constexpr (sizeof(X) == 4) return reinterpret_cast<const uint32_t *>(kt)[4 * (size_t)idx + 2];
+        else return reinterpret_cast<const uint64_t *>(kt)[4 * (size_t)idx + 2];
     }
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
     DEV X L2(int c) const { return c == 0 ? l2_0 : c == 1 ? l2_1 : c == 2 ? l2_2 : c == 3 ? l2_3 : l2_4; }
@@ -233,10 +249,56 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     int c0 = q[x];
     X ik0 = fm.L2(c0) + 1, ik2 = fm.L2(c0 + 1) - fm.L2(c0), ik1 = fm.L2(3 - c0) + 1;
     int ikend = x + 1;
-    int n = 0, i;
-    int qi = x + 1 < len ? q[x + 1] : 0;
+    int n = 0, i = x + 1;
     uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
-    for (i = x + 1; i < len; ++i) {
+    bool stop = false;               // the forward walk ended early (hole or interval below min_intv)
+    if constexpr (sizeof(X) == 4) {
+        // Lengths 2..min(K, len - x) come from the k-mer table.  Their table rows depend only on the read's
+        // bases, so every row is loaded before the first one is used (one round trip instead of K - 1);
+        // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
+        constexpr int KM = 11;   // kmer_depth() never exceeds 11
+        const int Lt = fm.K < len - x ? fm.K : len - x;
+        int cb[KM + 1];
+#pragma unroll
+        for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
+        uint2 e[KM + 1];
+        int nt = 1;   // bases from x covered without a hole (capped at Lt)
+#pragma unroll
+        for (int t = 2; t <= KM; ++t) {
+            if (nt == t - 1 && cb[t] < 4) {
+                fcode = fcode << 2 | (uint32_t)cb[t];
+                e[t] = reinterpret_cast<const uint2 *>(fm.kt)[2 * (size_t)(koff(t) + fcode)];
+                nt = t;
+            }
+        }
+        if (nt >= 2) {
+            nkm += (uint64_t)(nt - 1);
+            const X x1_last = fm.kget1(koff(nt) + fcode);
+#pragma unroll
+            for (int t = 2; t <= KM; ++t) {
+                if (t <= nt && !stop) {
+                    const X n0 = e[t].x, n2 = e[t].y;
+                    if (n2 != ik2) {
+                        if (n >= L.total()) { ovf = true; return len; }
+                        L.set(n++, ik0, ik2, ikend);
+                        if (n2 < (X)min_intv) { stop = true; i = x + t - 1; }
+                    }
+                    if (!stop) { ik0 = n0; ik2 = n2; ikend = x + t; }
+                }
+            }
+            ik1 = x1_last;
+        }
+        if (!stop) {
+            i = x + nt;
+            if (nt < Lt) {   // q[x + nt] is a hole: the walk stops there
+                if (n >= L.total()) { ovf = true; return len; }
+                L.set(n++, ik0, ik2, ikend);
+                stop = true;
+            }
+        }
+    }
+    int qi = !stop && i < len ? q[i] : 0;
+    for (; !stop && i < len; ++i) {
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;   // prefetch the next base
         if (cur < 4) {
@@ -295,9 +357,9 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
                 // strings q[i .. end) of at most K bases come from the k-mer table
                 const int La = pae - i, Lb = pbe - i;
                 const bool ta = La <= K, tb = hb && Lb <= K;
-                X ea0 = 0, ea1 = 0, ea2 = 0, eb0 = 0, eb1 = 0, eb2 = 0;
-                if (ta) fm.kget(koff(La) + (wcode >> (2 * (K - La))), ea0, ea1, ea2);
-                if (tb) fm.kget(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb1, eb2);
+                X ea0 = 0, ea2 = 0, eb0 = 0, eb2 = 0;
+                if (ta) fm.kget02(koff(La) + (wcode >> (2 * (K - La))), ea0, ea2);
+                if (tb) fm.kget02(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb2);
                 nkm += (uint64_t)ta + (uint64_t)tb;
                 if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
                 if (ta) { oa0 = ea0; oa2 = ea2; }
@@ -518,11 +580,11 @@ __global__ void k_kmer_level(DIndex ix, void *tabv, int L)
     const uint64_t P = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     auto put = [&](uint64_t idx, X a0, X a1, X a2) {
         if constexpr (sizeof(X) == 4) {
-            reinterpret_cast<uint4 *>(tabv)[idx] = make_uint4(a0, a1, a2, 0u);
+            reinterpret_cast<uint4 *>(tabv)[idx] = make_uint4(a0, a2, a1, 0u);
         } else {
             ulonglong2 *p = reinterpret_cast<ulonglong2 *>(tabv) + 2 * idx;
-            p[0] = make_ulonglong2(a0, a1);
-            p[1] = make_ulonglong2(a2, 0ull);
+            p[0] = make_ulonglong2(a0, a2);
+            p[1] = make_ulonglong2(a1, 0ull);
         }
     };
     if (L == 0) {
