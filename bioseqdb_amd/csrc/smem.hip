@@ -56,7 +56,12 @@ struct FM {
         else return reinterpret_cast<const uint64_t *>(kt)[4 * (size_t)idx + 2];
     }
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
-    DEV X L2(int c) const { return c == 0 ? l2_0 : c == 1 ? l2_1 : c == 2 ? l2_2 : c == 3 ? l2_3 : l2_4; }
+    // branch-free select (a nested conditional compiles to divergent branches around every extension)
+    DEV X L2(int c) const
+    {
+        const X a = (c & 1) ? l2_1 : l2_0, b = (c & 1) ? l2_3 : l2_2, r = (c & 2) ? b : a;
+        return (c & 4) ? l2_4 : r;
+    }
 };
 
 // rank of base c and of all bases > c in rows [0, k] (k = -1 -> 0), from a loaded occ block: the two
