@@ -681,6 +681,11 @@ struct EhRing {
     DEV void set(int j, int2 v) const { g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
 };
 
+// Query accessors whose values are pre-scaled codes (4 * code) with readable padding one column past either
+// end of every query window (QLane: the read staged in LDS): the cell score is then a 4-bit field of a
+// per-row profile word, and the next column is read without a bounds select.
+template <class QA> struct QPre { static constexpr bool v = false; };
+
 template <class EH, class QA>
 DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
                          int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
@@ -707,9 +712,14 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
     beg = 0, end = qlen;
     TStream ts;
     if (tlen > 0) ts.init(*target.ix, target.start, target.dir);
+    constexpr bool pre = QPre<QA>::v;
+    // profile of this row's target base: field q (4 bits at 4q) = score(tb, q) + 8 (pre-scaled path; the launch
+    // checks that every score of the matrix lies in [-8, 7])
+    const uint32_t prof_mis = (uint32_t)(sc.mis + 8) * 0x1111u | (uint32_t)(sc.amb + 8) << 16;
     for (i = 0; i < tlen; ++i) {
         int t, f = 0, h1, m = 0, mj = -1;
         const int tb = ts.next();
+        const uint32_t prof = prof_mis + ((uint32_t)(sc.match - sc.mis) << (4 * tb));   // tb < 4 (pac bases)
         if (beg < i - w) beg = i - w;
         if (end > i + w + 1) end = i + w + 1;
         if (end > qlen) end = qlen;
@@ -734,10 +744,11 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
             int qj = query(beg);
             for (j = beg; j < end; ++j) {
                 const int2 pn = eh.get(j + 1);
-                const int qn = j + 1 < end ? query(j + 1) : 0;
+                const int qn = pre ? query(j + 1) : (j + 1 < end ? query(j + 1) : 0);
                 int h, M = p.x, e = p.y;
                 const int hx = h1;
-                M = M ? M + sc(tb, qj) : 0;
+                if (pre) M = M ? M + (int)__builtin_amdgcn_ubfe(prof, (uint32_t)qj, 4u) - 8 : 0;
+                else M = M ? M + sc(tb, qj) : 0;
                 h = M > e ? M : e;
                 h = h > f ? h : f;
                 h1 = h;
@@ -1181,6 +1192,9 @@ struct QMakeL {
     int off;   // byte offset of this lane's column 0
     DEV QLane at(int start, int dir) const { return QLane{off, start, dir}; }
 };
+// k_extend<true> stages 4 * code; a window's one-past-the-end column (index -1 or len) lies inside the
+// dynamic LDS allocation (the ring precedes the query rows, one spare row follows them)
+template <> struct QPre<QLane> { static constexpr bool v = true; };
 
 // Extension rows for k_extend<true>: the eh row is a 64-column LDS ring (EhRing); the read is staged
 // in LDS once per read (QMakeL) after the ring columns.
@@ -1488,7 +1502,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
         if (LDS) {
             EhSmall ehx{(int)threadIdx.x, &X.ovf};   // blockDim == 64: lane-interleaved LDS columns
             const int qoff = 64 * EXT_LDS_COLS * 4 + (int)threadIdx.x;
-            for (int j = 0; j < len; ++j) g_lds_q8[qoff + j * 64] = q[j];   // stage the read in LDS
+            for (int j = 0; j < len; ++j) g_lds_q8[qoff + j * 64] = (uint8_t)(q[j] << 2);   // stage 4 * code in LDS
             QMakeL qm{qoff};
             for (int c = 0; c < nc && !X.ovf; ++c)
                 chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
@@ -1765,7 +1779,9 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     int wb = o.w;
     wb = std::min(wb, std::max(1, (int)((double)(cp.max_len * mx + end_bonus - o.o_ins) / o.e_ins + 1.)));
     wb = std::min(wb, std::max(1, (int)((double)(cp.max_len * mx + end_bonus - o.o_del) / o.e_del + 1.)));
-    const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 &&
+    auto in4 = [](int v) { return v >= -8 && v <= 7; };   // the profile's 4-bit score fields
+    const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 && in4(o.mat_match) && in4(o.mat_mismatch) &&
+                     in4(o.mat_amb) &&
                      (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     if (lds) {
         const size_t sh = (size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2);
