@@ -43,32 +43,38 @@ DEV int wave_excl_max(int v)
 // lane l receives v of lane l-1; lane 0 receives `first`
 DEV int wave_shr1(int v, int first) { return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false); }
 
-DEV int wave_sum(int v)
+// Scans and reductions over G consecutive lanes (a group; G = 64: the wave) with DPP: row_shr 1/2/4/8 within
+// each 16-lane row, row_bcast 15/31 across rows; lanes whose source is outside the group keep the identity.
+// (Cross-lane shuffles compile to ds_bpermute, an LDS round trip per step.)
+#define DPP_ID(op, v, id, ctrl, rmask) { const int u_ = __builtin_amdgcn_update_dpp(id, v, ctrl, rmask, 0xf, false); v = op(v, u_); }
+DEV int op_add(int a, int b) { return a + b; }
+DEV int op_min(int a, int b) { return a < b ? a : b; }
+DEV int op_max(int a, int b) { return a > b ? a : b; }
+template <int G, int (*OP)(int, int)> DEV int grp_scan(int v, int id)
 {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    DPP_ID(OP, v, id, 0x111, 0xf);
+    DPP_ID(OP, v, id, 0x112, 0xf);
+    DPP_ID(OP, v, id, 0x114, 0xf);
+    DPP_ID(OP, v, id, 0x118, 0xf);
+    if (G >= 32) DPP_ID(OP, v, id, 0x142, 0xa);   // row_bcast:15 into rows 1 and 3
+    if (G == 64) DPP_ID(OP, v, id, 0x143, 0xc);   // row_bcast:31 into rows 2 and 3
     return v;
 }
-
-// Scans over G consecutive lanes (a group; G = 64: the wave), generic shuffles.
-template <int G> DEV int grp_incl_sum(int v, int gl)
+// every lane of the group receives the group's last lane
+template <int G> DEV int grp_last(int v)
 {
-#pragma unroll
-    for (int d = 1; d < G; d <<= 1) { const int u = __shfl_up(v, d, G); if (gl >= d) v += u; }
-    return v;
+    if (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x15f, 0xf, 0xf, false);   // row_newbcast:15
+    if (G == 32) {
+        const int a = __builtin_amdgcn_readlane(v, 31), b = __builtin_amdgcn_readlane(v, 63);
+        return (threadIdx.x & 32) ? b : a;
+    }
+    return __builtin_amdgcn_readlane(v, 63);
 }
-template <int G> DEV int grp_incl_min(int v, int gl)
-{
-#pragma unroll
-    for (int d = 1; d < G; d <<= 1) { const int u = __shfl_up(v, d, G); if (gl >= d) v = v < u ? v : u; }
-    return v;
-}
-template <int G> DEV int grp_max_all(int v)
-{
-#pragma unroll
-    for (int off = G >> 1; off > 0; off >>= 1) { const int u = __shfl_xor(v, off, G); v = v > u ? v : u; }
-    return v;
-}
+template <int G> DEV int grp_incl_sum(int v, int) { return grp_scan<G, op_add>(v, 0); }
+template <int G> DEV int grp_incl_min(int v, int) { return grp_scan<G, op_min>(v, 0x7fffffff); }
+template <int G> DEV int grp_max_all(int v) { return grp_last<G>(grp_scan<G, op_max>(v, NEG_SCAN)); }
+template <int G> DEV int grp_sum(int v) { return grp_last<G>(grp_scan<G, op_add>(v, 0)); }
+DEV int wave_sum(int v) { return grp_sum<64>(v); }
 
 // The exact form of diagonal_wins (dev_common.h) for the diagonals it cannot decide: with diagonal score S,
 // every path through ksw_global2's n x n matrix other than the diagonal has either
@@ -105,10 +111,10 @@ DEV bool detour_free(const DOpts &o, const Score sc, int n, int S, TQ tq, int gl
             x = x > a1 ? x : a1;
             x = x > am ? x : am;
         }
-        c1 += __shfl(i1, G - 1, G);
-        cm += __shfl(im, G - 1, G);
-        m1 = __shfl(n1, G - 1, G);
-        mm = __shfl(nm, G - 1, G);
+        c1 += grp_last<G>(i1);
+        cm += grp_last<G>(im);
+        m1 = grp_last<G>(n1);
+        mm = grp_last<G>(nm);
     }
     x = grp_max_all<G>(x);
     return (int64_t)x < (int64_t)(o.o_ins + o.e_ins + o.o_del + o.e_del);
@@ -562,12 +568,6 @@ template <int G> DEV int grp_shl1(int v, int last, int gl)
     if (G == 16) return __builtin_amdgcn_update_dpp(last, v, 0x101, 0xf, 0xf, false);
     const int sv = __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
     return gl == G - 1 ? last : sv;
-}
-template <int G> DEV int grp_sum(int v)
-{
-#pragma unroll
-    for (int off = G >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, G);
-    return v;
 }
 
 // ksw_global2 (global mode) for bands of at most G columns: rows as in ksw_global2_reg; target and
