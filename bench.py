@@ -265,6 +265,8 @@ def main() -> int:
                     help="concurrent batches per GPU (bsq_batch_run_many); each aligns 1/S of the reads")
     ap.add_argument("--index-build", default="device", choices=["device", "host"],
                     help="where the index is built before the timed region (device: bsq_index_build_device)")
+    ap.add_argument("--exchange-world1", action="store_true",
+                    help="run the N > 1 exchange path with a process group of one rank (tests it on a one-GPU box)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
@@ -281,7 +283,7 @@ def main() -> int:
     dist = None
     gpu = local
     xdev = None   # device of the exchange tensors
-    if world > 1:
+    if world > 1 or args.exchange_world1:
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()   # does not initialise the GPU
@@ -367,21 +369,40 @@ def main() -> int:
             N.check(L.bsq_batch_run(batch, ctypes.byref(opts), first_call))
         else:
             N.check(L.bsq_batch_run_many(b_arr, S, ctypes.byref(opts), fc_arr))
-        if dist is not None:   # exchange step: hit records + CIGARs of every rank to the caller
-            import torch
-            from bioseqdb_amd import dist as D
-            parts = []
-            for b in batches:   # batch order == read order
-                H = L.bsq_batch_hits(b).contents
-                nb = H.n_hits * ctypes.sizeof(N.Hit)
-                nc = H.n_cigar * 4
-                parts.append(np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb])
-                parts.append(np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc])
-            D.gather_records(np.concatenate(parts), device=xdev)
+        if dist is not None:   # exchange step: hit records + CIGARs of every rank to the caller (rank 0)
+            if xchg.gpu:   # device records straight into the RCCL send buffer; the gather overlaps the next step
+                sz = []
+                for b in batches:   # batch order == read order
+                    nb = ctypes.c_int64()
+                    N.check(L.bsq_batch_copy_records(b, None, 0, ctypes.byref(nb)))
+                    sz.append(nb.value)
 
+                def fill(send):
+                    off = 0
+                    for b, nb in zip(batches, sz):
+                        got = ctypes.c_int64()
+                        N.check(L.bsq_batch_copy_records(b, ctypes.c_void_p(send.data_ptr() + off), nb, ctypes.byref(got)))
+                        off += nb
+                xchg.post_fill(sum(sz), fill)
+            else:
+                parts = []
+                for b in batches:
+                    H = L.bsq_batch_hits(b).contents
+                    nb = H.n_hits * ctypes.sizeof(N.Hit)
+                    nc = H.n_cigar * 4
+                    parts.append(np.ctypeslib.as_array(ctypes.cast(H.hits, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))[:nb])
+                    parts.append(np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc])
+                xchg.post(parts)
+
+    xchg = None
+    if dist is not None:
+        from bioseqdb_amd import dist as D
+        xchg = D.RecordExchange(device=xdev)
     hb.phase = "aligning"
     for _ in range(args.warmup):
         step()
+    if xchg is not None:
+        xchg.finish()
     stage_ms = np.zeros(6)
     stage_bytes = np.zeros(6)
     stage_work = np.zeros(6)
@@ -404,6 +425,7 @@ def main() -> int:
             stage_bytes += np.array(list(by))
     if dist is not None:
         import torch
+        xchg.finish()   # the last step's records are on the caller's host
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -466,6 +488,11 @@ def main() -> int:
             "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
             "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
             "streams": S, "reads_per_launch": int(round(reads_per_launch)),
+        },
+        "exchange": None if xchg is None else {
+            "path": ("RCCL gather of device records to rank 0, pinned D2H there, overlapped with the next step"
+                     if xchg.gpu else "gloo gather of host records to rank 0 (rehearsal)"),
+            "bytes_per_step_rank0": int(xchg.bytes_moved / max(args.steps + args.warmup, 1)) if rank == 0 else None,
         },
         "roofline": {
             "bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -106,6 +106,7 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                            ctypes.POINTER(ctypes.c_int64)]),
     "bsq_batch_retried": (ctypes.c_int64, [_P]),
+    "bsq_batch_copy_records": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "bsq_index_build_device": (ctypes.c_int, [_P, ctypes.c_int]),
     "bsq_batch_run_many": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(Opts),
                                           ctypes.POINTER(ctypes.c_uint64)]),

@@ -840,6 +840,7 @@ struct bsq_batch {
     double stage_bytes[STG_N]{};
     double stage_work[STG_N]{};
     int64_t retried = 0;
+    bool dev_whole = false;   // d_out / d_out_cig hold the whole last run's view (one chunk, no retried read)
 };
 
 static const char *kStageNames[STG_N] = {"smem", "chain", "extend", "reg2aln", "pack", "d2h"};
@@ -1389,6 +1390,7 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     }
     // the results stay in the batch-wide pinned arrays (zero-copy view, valid until the next run)
     if (n == 0 || b->idx->h.seq_len == 0) for (int r = 0; r <= n; ++r) b->h_pinned_off[r] = 0;
+    b->dev_whole = n > 0 && b->chunk >= n && b->retried == 0 && b->idx->h.seq_len > 0;
     b->view.n_reads = n;
     b->view.n_hits = hit_total;
     b->view.hits = b->h_pinned;
@@ -1567,6 +1569,27 @@ extern "C" int bsq_batch_intervals(bsq_batch *b, const int64_t **read_off, const
     *read_off = b->seed_off.data();
     *intv = b->seed_intv.data();
     *n_intv = b->seed_off[n];
+    return BSQ_OK;
+}
+
+// The last run's records as one byte range in device memory (hits, then CIGAR words) -- the exchange step's
+// send buffer of a sharded job (bench.py --gpus N): straight from the packed device arrays when they hold the
+// whole view (one chunk, no retried read), else from the pinned host view.  dst == nullptr: size query.
+extern "C" int bsq_batch_copy_records(const bsq_batch *b, void *dst, int64_t cap, int64_t *bytes)
+{
+    if (!b || !bytes) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    const int64_t nh = b->view.n_hits * (int64_t)sizeof(bsq_hit), nc = b->view.n_cigar * 4;
+    *bytes = nh + nc;
+    if (!dst || nh + nc == 0) return BSQ_OK;
+    if (cap < nh + nc) { set_err("destination holds %lld bytes, records need %lld", (long long)cap, (long long)(nh + nc)); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    const hipMemcpyKind k = b->dev_whole ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const void *sh = b->dev_whole ? (const void *)b->d_out : (const void *)b->view.hits;
+    const void *sc = b->dev_whole ? (const void *)b->d_out_cig : (const void *)b->view.cigar;
+    uint8_t *d = static_cast<uint8_t *>(dst);
+    if (nh) HIPCHK(hipMemcpyAsync(d, sh, (size_t)nh, k, b->stream));
+    if (nc) HIPCHK(hipMemcpyAsync(d + nh, sc, (size_t)nc, k, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
     return BSQ_OK;
 }
 

@@ -50,6 +50,121 @@ def gather_records(local: np.ndarray, group=None, device=None, dst: int = 0) -> 
     return [o[:s].cpu().numpy() for o, s in zip(out, sizes_i)]
 
 
+class RecordExchange:
+    """The exchange step of a sharded job, pipelined (bench.py --gpus N): the hit records
+    of step k travel to rank `dst` (the calling backend) while step k+1 aligns.
+
+    post(parts) takes this rank's record segments of one step (host uint8 arrays, in read order):
+      * the byte counts are all-gathered (tiny, host-visible: the receive buffers are sized from them);
+      * the segments are packed into this rank's send buffer -- in HBM for RCCL (host-to-device copies on a side
+        stream), in host memory for gloo -- and gathered into `dst`'s receive buffers asynchronously (RCCL over
+        xGMI on a multi-GPU node);
+      * on `dst` the received buffers are copied into pinned host memory after the gather (same side stream), so
+        the rows reach the caller's host without a host-side wait in the step.
+    post() first completes the previous exchange (its buffers are reused); finish() completes the last one.
+    result() on `dst` returns the per-rank byte arrays of the last completed exchange, in rank (= read) order.
+    """
+
+    def __init__(self, device=None, group=None, dst: int = 0):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group, self.dst = torch, dist, group, dst
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.dev = device if device is not None else torch.device("cpu")
+        self.gpu = self.dev.type == "cuda"
+        self.stream = torch.cuda.Stream(device=self.dev) if self.gpu else None
+        self.send = None
+        self.recv = None
+        self.host = None
+        self.work = None
+        self.event = None
+        self.sizes = None
+        self.done_sizes = None
+        self.bytes_moved = 0
+
+    def _grow(self, buf, n, pinned_host=False):
+        torch = self.torch
+        if buf is not None and buf.numel() >= n:
+            return buf
+        n = max(int(n * 1.25), 1)
+        if pinned_host:
+            return torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        return torch.empty(n, dtype=torch.uint8, device=self.dev)
+
+    def post(self, parts: Sequence[np.ndarray]) -> None:
+        """Exchange host record segments (read order)."""
+        torch = self.torch
+
+        def fill(send):
+            off = 0
+            for p in parts:
+                if p.nbytes:
+                    src = torch.from_numpy(np.ascontiguousarray(p).view(np.uint8).reshape(-1))
+                    send[off:off + p.nbytes].copy_(src)
+                    off += p.nbytes
+        self.post_fill(int(sum(p.nbytes for p in parts)), fill)
+
+    def post_fill(self, n: int, fill) -> None:
+        """Exchange n bytes that fill(send_buffer) writes into bytes [0, n) of the send buffer (on this rank's
+        exchange device) and that are complete when it returns (e.g. bsq_batch_copy_records per batch)."""
+        torch, dist = self.torch, self.dist
+        self.finish()
+        cnt = torch.tensor([n], dtype=torch.int64, device=self.dev)
+        allc = [torch.zeros(1, dtype=torch.int64, device=self.dev) for _ in range(self.world)]
+        dist.all_gather(allc, cnt, group=self.group)
+        sizes = [int(c.item()) for c in allc]
+        mx = max(max(sizes), 1)
+        self.send = self._grow(self.send, mx)
+        me_dst = self.rank == self.dst
+        if me_dst:
+            if self.recv is None or len(self.recv) != self.world or self.recv[0].numel() < mx:
+                self.recv = [self._grow(None, mx) for _ in range(self.world)]
+            if self.gpu and (self.host is None or any(h.numel() < s for h, s in zip(self.host, sizes))):
+                self.host = [self._grow(None, max(s, 1), pinned_host=True) for s in sizes]
+        if self.gpu:
+            torch.cuda.current_stream(self.dev).synchronize()   # the send buffer's allocation / last use
+        fill(self.send)
+        ctx = torch.cuda.stream(self.stream) if self.gpu else _nullctx()
+        with ctx:
+            recv = [r[:mx] for r in self.recv] if me_dst else None
+            self.work = dist.gather(self.send[:mx], recv, dst=self.dst, group=self.group, async_op=True)
+            if me_dst and self.gpu:
+                self.work.wait()   # orders the side stream after the gather, without a host wait
+                for h, r, s in zip(self.host, self.recv, sizes):
+                    if s:
+                        h[:s].copy_(r[:s], non_blocking=True)
+            if self.gpu:
+                self.event = torch.cuda.Event()
+                self.event.record(self.stream)
+        self.sizes = sizes
+        self.bytes_moved += sum(sizes) if me_dst else n
+
+    def finish(self) -> None:
+        if self.work is None:
+            return
+        self.work.wait()
+        if self.event is not None:
+            self.event.synchronize()
+        self.work, self.event = None, None
+        self.done_sizes = self.sizes
+
+    def result(self) -> List[np.ndarray]:
+        """`dst`: the per-rank record bytes of the last finished exchange (valid until the next post); else []."""
+        if self.rank != self.dst or self.done_sizes is None:
+            return []
+        bufs = self.host if self.gpu else self.recv
+        return [b[:s].numpy() for b, s in zip(bufs, self.done_sizes)]
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def replicate_index(L, idx, gpu: int, src: int = 0, group=None):
     """One index build for the whole job: rank `src` passes its built host index
     `idx`, every other rank passes None.  The root uploads into torch-allocated device buffers, the

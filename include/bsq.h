@@ -247,6 +247,10 @@ int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **
 int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
+/* The last run's records as bytes in device memory on the batch's device: the bsq_hit array, then the CIGAR
+   words (the exchange step's send buffer of a read-sharded multi-GPU job; the caller-side receive of
+   extension.cpp:362-370's rows).  dst == NULL returns the size in *bytes.  BSQ_E_INVALID when cap is short. */
+int bsq_batch_copy_records(const bsq_batch *b, void *dst, int64_t cap, int64_t *bytes);
 /* Per-stage device time of the last run in ms, measured with HIP events on the batch stream.
  * Writes up to `max` values; returns the number of stages; names via bsq_stage_name(). */
 int bsq_batch_stage_ms(const bsq_batch *b, float *ms, int max);

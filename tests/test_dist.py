@@ -57,6 +57,45 @@ def test_gather_records_world2_gloo():
             assert got == [], rank            # only the calling backend receives rows
 
 
+def _xchg_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = D.RecordExchange()
+    out = []
+    for step in range(4):   # ragged per-rank, per-step record bytes in 1-3 segments
+        rng = np.random.default_rng(100 * step + rank)
+        parts = [rng.integers(0, 255, size=int(rng.integers(0, 5000)), dtype=np.uint8) for _ in range(1 + (step + rank) % 3)]
+        x.post(parts)   # completes the previous step's exchange first
+        q.put(("sent", rank, step, b"".join(p.tobytes() for p in parts)))
+        x.finish()
+        out.append([r.tobytes() for r in x.result()])
+    q.put(("got", rank, out))
+    dist.destroy_process_group()
+
+
+def test_record_exchange_pipelined_world3_gloo():
+    """RecordExchange (the bench's pipelined exchange step): after each finish, rank 0 holds every rank's bytes of
+    that step in rank order; other ranks hold nothing."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_xchg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    msgs = [q.get(timeout=120) for _ in range(world * 5)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sent = {(m[1], m[2]): m[3] for m in msgs if m[0] == "sent"}
+    got = {m[1]: [o for o in m[2] if o != []] for m in msgs if m[0] == "got"}
+    assert all(got[r] == [] for r in range(1, world))
+    assert len(got[0]) == 4
+    for step in range(4):
+        assert got[0][step] == [sent[(r, step)] for r in range(world)]
+
+
 def test_merge_rows():
     assert D.merge_rows([[(1,), (2,)], [], [(3,)]]) == [(1,), (2,), (3,)]
 
