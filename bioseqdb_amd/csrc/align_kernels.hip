@@ -742,6 +742,7 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
         if (beg < end) {
             int2 p = eh.get(beg);
             int qj = query(beg);
+#pragma unroll 2   // two cells per trip: no loop-carried register copies, half the loop control (42 -> 36 per cell)
             for (j = beg; j < end; ++j) {
                 const int2 pn = eh.get(j + 1);
                 const int qn = pre ? query(j + 1) : (j + 1 < end ? query(j + 1) : 0);
