@@ -56,6 +56,18 @@ struct FM {
         else return reinterpret_cast<const uint64_t *>(kt)[4 * (size_t)idx + 2];
     }
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
+    // the text T = pac || revcomp(pac) and its suffix array, for walking a unique interval along the text
+    const uint8_t *pac;
+    int64_t l_pac;
+    const uint32_t *sa32;
+    const uint64_t *sa64;
+    DEV int64_t sa(X row) const { return sa64 ? (int64_t)sa64[row] : (int64_t)sa32[row]; }
+    DEV int tbase(int64_t t) const
+    {
+        const int64_t f = t < l_pac ? t : (l_pac << 1) - 1 - t;
+        const int b = (pac[f >> 2] >> ((~f & 3) << 1)) & 3;
+        return t < l_pac ? b : 3 - b;
+    }
     // branch-free select (a nested conditional compiles to divergent branches around every extension)
     DEV X L2(int c) const
     {
@@ -304,6 +316,26 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     }
     int qi = !stop && i < len ? q[i] : 0;
     for (; !stop && i < len; ++i) {
+        if (ik2 == 1 && min_intv <= 1) {
+            // A unique interval [x0, x0] stays [x0, x0] while the string extends along its one occurrence at
+            // SA[x0] (the row of that suffix does not move) and becomes empty at the first base that differs
+            // from the text (or at the text's end): walk the text instead of one rank query per base.  x[1]
+            // is not read again by bwt_smem1 once the forward walk ends.
+            const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
+            int k = i;
+            while (k < len) {
+                const int c = q[k];
+                if (c > 3 || p + k >= nT || fm.tbase(p + k) != c) break;
+                ++k;
+            }
+            ikend = k;
+            i = k;
+            if (k < len) {   // a differing base or a hole: the interval is pushed and the walk stops
+                if (n >= L.total()) { ovf = true; return len; }
+                L.set(n++, ik0, ik2, ikend);
+            }
+            break;
+        }
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;   // prefetch the next base
         if (cur < 4) {
@@ -478,6 +510,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     fm.primary = (X)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
     fm.K = ix.kmer_k;   // the table is built in the index's row width
+    fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
     uint64_t nblk = 0, nkm = 0;
     const int li = blockIdx.x * T + t;
     if (li < n) {
