@@ -323,10 +323,21 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
             // is not read again by bwt_smem1 once the forward walk ends.
             const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
             int k = i;
-            while (k < len) {
-                const int c = q[k];
-                if (c > 3 || p + k >= nT || fm.tbase(p + k) != c) break;
-                ++k;
+            for (;;) {   // 8 bases per trip: all 16 loads issued before the first compare
+                constexpr int W = 8;
+                int qc[W], tc[W];
+#pragma unroll
+                for (int t = 0; t < W; ++t) {
+                    const bool in = k + t < len && p + k + t < nT;
+                    qc[t] = in ? q[k + t] : 5;
+                    tc[t] = in ? fm.tbase(p + k + t) : 4;
+                }
+                int r = W;
+#pragma unroll
+                for (int t = W - 1; t >= 0; --t)
+                    if (qc[t] != tc[t]) r = t;   // holes (> 3) never equal a text base; past the end 5 != 4
+                k += r;
+                if (r < W) break;
             }
             ikend = k;
             i = k;
