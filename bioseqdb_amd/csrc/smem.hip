@@ -387,12 +387,16 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     const int K = fm.K;
     uint32_t wcode = 0;   // q[i .. i+K) packed, first base most significant (positions past the read: 0)
     for (int t = 0; t < K; ++t) wcode = wcode << 2 | (x + t < len ? (uint32_t)(q[x + t] & 3) : 0u);
-    for (i = x - 1; i >= -1; --i) {
-        const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
-        if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
-        int nc = 0;
-        X last_x2 = 0;
-        for (int j = 0; j < n; j += 2) {
+    // One flat loop over (position i, entry pair j): a lane whose list at i is exhausted moves on to i - 1
+    // in the same trip instead of waiting for the lane with the longest list (the nest's inner loop ran
+    // to the wave's largest n at every i).  Per lane the order of work is the nest's.
+    i = x - 1;
+    int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+    if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
+    int nc = 0, j = 0;
+    X last_x2 = 0;
+    for (;;) {
+        {
             // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
             // Compaction writes go to nc <= j, below both entries already read.
             const bool hb = j + 1 < n;
@@ -433,8 +437,14 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
                 }
             }
         }
-        if (nc == 0) break;
-        n = nc;
+        j += 2;
+        if (j >= n) {   // position i done (at i = -1 every entry is a hit, so nc == 0 ends the loop there)
+            if (nc == 0) break;
+            n = nc; nc = 0; j = 0; last_x2 = 0;
+            --i;
+            c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+            if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
+        }
     }
     return ret;
 }
