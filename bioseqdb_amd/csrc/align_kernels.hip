@@ -269,15 +269,15 @@ __global__ void __launch_bounds__(256) k_smem(DIndex ix, DOpts o, Caps cp, const
 // klib ks_introsort (ksort.h) over an index array; lt(x, y) compares element ids.  The pivot,
 // partition and final insertion sort follow klib exactly, so ties land where libbwa puts them.
 // ------------------------------------------------------------------------------------------------
-template <class LT>
-DEV void ks_insertsort(int *a, int n, LT lt)
+template <class A, class LT>
+DEV void ks_insertsort(A a, int n, LT lt)
 {
     for (int i = 1; i < n; ++i)
         for (int j = i; j > 0 && lt(a[j], a[j - 1]); --j) { int t = a[j]; a[j] = a[j - 1]; a[j - 1] = t; }
 }
 
-template <class LT>
-DEV void ks_combsort(int *a, int n, LT lt)
+template <class A, class LT>
+DEV void ks_combsort(A a, int n, LT lt)
 {
     const double shrink_factor = 1.2473309501039786540366528676643;
     int do_swap;
@@ -298,8 +298,8 @@ DEV void ks_combsort(int *a, int n, LT lt)
 
 // stk: 3 x 64 ints of the thread's global scratch (the partition stack, touched only by partitions of more
 // than 16 elements): a private array here would give every wave of the kernel a scratch segment
-template <class LT>
-DEV void ks_introsort(int *a, int n, LT lt, int *stk)
+template <class A, class LT, class S>
+DEV void ks_introsort(A a, int n, LT lt, S stk)
 {
     if (n < 1) return;
     if (n == 2) {
@@ -308,7 +308,8 @@ DEV void ks_introsort(int *a, int n, LT lt, int *stk)
     }
     int d;
     for (d = 2; (1ul << d) < (unsigned long)n; ++d);
-    int *stk_l = stk, *stk_r = stk + 64, *stk_d = stk + 128, top = 0;
+    S stk_l = stk, stk_r = stk + 64, stk_d = stk + 128;
+    int top = 0;
     int s = 0, t = n - 1;
     d <<= 1;
     while (1) {
@@ -348,15 +349,23 @@ DEV void ks_introsort(int *a, int n, LT lt, int *stk)
 // ------------------------------------------------------------------------------------------------
 // k_chain: mem_chain (kbtree t = 5, KB_DEFAULT_SIZE 512) + mem_chain_flt
 // ------------------------------------------------------------------------------------------------
+// The chaining state is lane-private but lives in global scratch.  Element i of a lane's array sits at
+// [i * 64 + lane] of its wave's region (SP below), so when the lanes of a wave touch the same element
+// index the accesses fall on adjacent addresses instead of 64 separate per-lane areas.
+template <typename T> struct SP {
+    T *p;
+    DEV T &operator[](int i) const { return p[(size_t)i * 64]; }
+    DEV SP operator+(int i) const { return SP{p + (size_t)i * 64}; }
+};
 struct SeedNode { int64_t rbeg; int32_t qbeg, len, next, pad; };
 struct ChainNode { int64_t pos; int32_t rid, n, head, tail, w, kept, first, pad; };
 struct KNode { int32_t n, is_internal; int32_t key[9]; int32_t ptr[10]; };
 #define KB_T 5
 
 struct ChainCtx {
-    SeedNode *seeds; int n_seeds, cap_seeds;
-    ChainNode *ch; int n_ch, cap_ch;
-    KNode *nodes; int n_nodes, cap_nodes;
+    SP<SeedNode> seeds; int n_seeds, cap_seeds;
+    SP<ChainNode> ch; int n_ch, cap_ch;
+    SP<KNode> nodes; int n_nodes, cap_nodes;
     int root, n_keys;
     bool ovf;
 };
@@ -500,17 +509,23 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t nsa = 0;
-    uint8_t *sb = scratch + (size_t)tid * cp.scratch;
+    // this wave's 64 * cp.scratch bytes: each array lane-interleaved (SP); the workspace holds whole waves
+    const int lane = tid & 63;
+    uint8_t *wb = scratch + (size_t)(tid >> 6) * 64 * (size_t)cp.scratch;
     ChainCtx C;
-    C.seeds = reinterpret_cast<SeedNode *>(sb);
     C.cap_seeds = cp.seeds;
-    C.ch = reinterpret_cast<ChainNode *>(sb + (size_t)cp.seeds * sizeof(SeedNode));
     C.cap_ch = cp.chains;
-    C.nodes = reinterpret_cast<KNode *>(sb + (size_t)cp.seeds * sizeof(SeedNode) + (size_t)cp.chains * sizeof(ChainNode));
     C.cap_nodes = cp.chains / 2 + 8;
-    int *ord = reinterpret_cast<int *>(reinterpret_cast<uint8_t *>(C.nodes) + (size_t)C.cap_nodes * sizeof(KNode));
-    int *kept_list = ord + cp.chains;
-    int *stk = kept_list + cp.chains;      // introsort stack (192 ints), then the B-tree walk's (3 x 24)
+    size_t off = 0;
+    C.seeds = SP<SeedNode>{reinterpret_cast<SeedNode *>(wb) + lane};
+    off += (size_t)C.cap_seeds * 64 * sizeof(SeedNode);
+    C.ch = SP<ChainNode>{reinterpret_cast<ChainNode *>(wb + off) + lane};
+    off += (size_t)C.cap_ch * 64 * sizeof(ChainNode);
+    C.nodes = SP<KNode>{reinterpret_cast<KNode *>(wb + off) + lane};
+    off += (size_t)C.cap_nodes * 64 * sizeof(KNode);
+    SP<int> ord{reinterpret_cast<int *>(wb + off) + lane};
+    SP<int> kept_list = ord + cp.chains;
+    SP<int> stk = kept_list + cp.chains;   // introsort stack (192 ints), then the B-tree walk's (3 x 24)
     for (int li = tid; li < n; li += nthr) {
         n_chains[li] = 0;
         if (status[li]) continue;
@@ -555,7 +570,8 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         // in-order traversal of the B-tree -> chain order
         int nord = 0;
         {   // iterative in-order walk == kbtree's __kb_traverse
-            int *stn = stk + 192, *sti = stn + 24, *std_ = sti + 24, sp = 0;
+            SP<int> stn = stk + 192, sti = stn + 24, std_ = sti + 24;
+            int sp = 0;
             stn[0] = C.root; sti[0] = 0; std_[0] = 0;
             if (!C.nodes[C.root].is_internal) {   // a lone leaf root (<= 9 chains, the common case): its keys
                 const KNode &nd = C.nodes[C.root];
@@ -584,7 +600,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
             if (c.w >= o.min_chain_weight) ord[n_chn++] = ord[i];
         }
         if (n_chn > 0) {
-            ChainNode *ch = C.ch;
+            const SP<ChainNode> ch = C.ch;
             ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; }, stk);
             ch[ord[0]].kept = 3;
             int nk = 0;

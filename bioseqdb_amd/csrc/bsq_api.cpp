@@ -738,7 +738,8 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     // Every stage kernel derives its scratch pointer from the thread id but dereferences it only inside
     // `for (li = tid; li < n; ...)`; a retry workspace runs n <= max_reads reads per launch, so only
     // max_reads threads ever touch scratch (the main pass may run more reads than threads: full grid).
-    w.scratch_total = (with_sel ? (int64_t)std::max(max_reads, 1) : (int64_t)w.grid * 256) * w.cp.scratch;
+    // (k_chain lays its state out per wave of 64 threads: whole waves)
+    w.scratch_total = (with_sel ? ((int64_t)std::max(max_reads, 1) + 63) / 64 * 64 : (int64_t)w.grid * 256) * w.cp.scratch;
     HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
     if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
     if (long_reads(cp.max_len)) HIPCHK(hipMalloc(&w.sscore, R * cp.seeds * 4));
