@@ -34,8 +34,12 @@ def _raise(rc: int) -> None:
 
 
 def _take(ptr: ctypes.c_void_p, nbytes: int) -> bytes:
+    # (ctypes.string_at takes a C int size: texts of 2 GiB and more are copied through a sized array)
     try:
-        return ctypes.string_at(ptr, nbytes) if nbytes else b""
+        if not nbytes:
+            return b""
+        addr = ptr.value if isinstance(ptr, ctypes.c_void_p) else ptr
+        return bytes((ctypes.c_char * nbytes).from_address(addr))
     finally:
         lib().bsq_free(ptr)
 
