@@ -93,8 +93,9 @@ DEV uint64_t sa_at(const DIndex &ix, uint64_t row) { return ix.sa32 ? (uint64_t)
 // ------------------------------------------------------------------------------------------------
 // bounded vectors in private scratch
 // ------------------------------------------------------------------------------------------------
-struct IV {
-    Intv *a;
+template <class P>
+struct IVT {
+    P a;
     int n, cap;
     DEV bool push(const Intv &v, bool &ovf)
     {
@@ -107,6 +108,7 @@ struct IV {
         for (int j = 0; j < (n >> 1); ++j) { Intv t = a[n - 1 - j]; a[n - 1 - j] = a[j]; a[j] = t; }
     }
 };
+using IV = IVT<Intv *>;
 
 // bwt_smem1a with max_intv = 0 (bwt_smem1)
 DEVN int smem1(const DIndex &ix, int len, const uint8_t *q, int x, int min_intv, IV &mem, IV &va, IV &vb,
@@ -212,7 +214,7 @@ __global__ void __launch_bounds__(256) k_smem(DIndex ix, DOpts o, Caps cp, const
         const uint8_t *q = codes + offs[r];
         const int len = (int)(offs[r + 1] - offs[r]);
         bool ovf = false;
-        IV mem{intv_out + (size_t)li * cp.intv, 0, cp.intv};
+        IVT<SP<Intv>> mem{SP<Intv>{intv_out + intv_slot_at_d(li, 0, cp.intv)}, 0, cp.intv};
         IV mem1{sbase, 0, vcap}, va{sbase + vcap, 0, vcap}, vb{sbase + 2 * vcap, 0, vcap};
         const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
         int x = 0;
@@ -352,11 +354,6 @@ DEV void ks_introsort(A a, int n, LT lt, S stk)
 // The chaining state is lane-private but lives in global scratch.  Element i of a lane's array sits at
 // [i * 64 + lane] of its wave's region (SP below), so when the lanes of a wave touch the same element
 // index the accesses fall on adjacent addresses instead of 64 separate per-lane areas.
-template <typename T> struct SP {
-    T *p;
-    DEV T &operator[](int i) const { return p[(size_t)i * 64]; }
-    DEV SP operator+(int i) const { return SP{p + (size_t)i * 64}; }
-};
 struct SeedNode { int64_t rbeg; int32_t qbeg, len, next, pad; };
 struct ChainNode { int64_t pos; int32_t rid, n, head, tail, w, kept, first, pad; };
 struct KNode { int32_t n, is_internal; int32_t key[9]; int32_t ptr[10]; };
@@ -534,7 +531,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         if (len < o.min_seed_len) continue;
         C.n_seeds = 0; C.n_ch = 0; C.n_nodes = 0; C.n_keys = 0; C.ovf = false;
         C.root = kb_new_node(C);
-        const Intv *mem = intv + (size_t)li * cp.intv;
+        const SP<const Intv> mem{intv + intv_slot_at_d(li, 0, cp.intv)};
         const int nm = n_intv[li];
         for (int i = 0; i < nm && !C.ovf; ++i) {
             const Intv p = mem[i];
@@ -1702,7 +1699,7 @@ __global__ void k_intv_pack(int n, int cap, const Intv *__restrict__ slots, cons
 {
     const int li = blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= n || status[li]) return;
-    const Intv *a = slots + (size_t)li * cap;
+    const SP<const Intv> a{slots + intv_slot_at_d(li, 0, cap)};
     uint64_t *d = out + 4 * (size_t)off[li];
     for (int k = 0; k < n_intv[li]; ++k) {
         d[4 * k + 0] = a[k].x[0]; d[4 * k + 1] = a[k].x[1]; d[4 * k + 2] = a[k].x[2]; d[4 * k + 3] = a[k].info;

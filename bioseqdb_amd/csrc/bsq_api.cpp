@@ -725,7 +725,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     w.grid = (threads + 255) / 256;
     const size_t R = (size_t)std::max(max_reads, 1);
     HIPCHK(hipMalloc(&w.status, R * 4));
-    HIPCHK(hipMalloc(&w.intv, R * cp.intv * sizeof(Intv)));
+    HIPCHK(hipMalloc(&w.intv, (size_t)intv_slot_reads((int64_t)R) * cp.intv * sizeof(Intv)));   // whole waves
     HIPCHK(hipMalloc(&w.n_intv, R * 4));
     HIPCHK(hipMalloc(&w.n_chains, R * 4));
     HIPCHK(hipMalloc(&w.n_regs, R * 4));
@@ -1432,7 +1432,7 @@ static int seed_chunk(bsq_batch *b, const DOpts &o, int n)
             const int CH = retry_chunk(level);
             std::vector<int32_t> cnt((size_t)CH), next;
             std::vector<uint32_t> stt((size_t)CH);
-            std::vector<Intv> slots((size_t)CH * r.cp.intv);
+            std::vector<Intv> slots((size_t)intv_slot_reads(CH) * r.cp.intv);
             for (size_t s0 = 0; s0 < pend.size(); s0 += (size_t)CH) {
                 const int m = (int)std::min<size_t>((size_t)CH, pend.size() - s0);
                 HIPCHK(hipMemcpyAsync(r.sel, pend.data() + s0, (size_t)m * 4, hipMemcpyHostToDevice, st));
@@ -1440,7 +1440,8 @@ static int seed_chunk(bsq_batch *b, const DOpts &o, int n)
                 { const int rc = seed_stage(b, r, o, m, r.sel); if (rc) return rc; }
                 HIPCHK(hipMemcpyAsync(cnt.data(), r.n_intv, (size_t)m * 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipMemcpyAsync(stt.data(), r.status, (size_t)m * 4, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipMemcpyAsync(slots.data(), r.intv, (size_t)m * r.cp.intv * sizeof(Intv), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(slots.data(), r.intv, (size_t)intv_slot_reads(m) * r.cp.intv * sizeof(Intv),
+                                      hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 for (int j = 0; j < m; ++j) {
                     if (stt[(size_t)j]) {
@@ -1450,7 +1451,7 @@ static int seed_chunk(bsq_batch *b, const DOpts &o, int n)
                     }
                     std::vector<uint64_t> v((size_t)cnt[(size_t)j] * 4);
                     for (int k = 0; k < cnt[(size_t)j]; ++k) {
-                        const Intv &x = slots[(size_t)j * r.cp.intv + k];
+                        const Intv &x = slots[(size_t)intv_slot_at(j, k, r.cp.intv)];
                         v[4 * k] = x.x[0]; v[4 * k + 1] = x.x[1]; v[4 * k + 2] = x.x[2]; v[4 * k + 3] = x.info;
                     }
                     b->seed_retry.emplace_back(pend[s0 + (size_t)j], std::move(v));

@@ -24,6 +24,22 @@ struct alignas(32) OccBlock32 {
 };
 static_assert(sizeof(OccBlock32) == 32, "occ32 block must be 32 bytes");
 
+// Per-read interval slots (cap entries each) are laid out by wave of 64 reads: entry k of read li sits at
+// [((li / 64) * cap + k) * 64 + li % 64], so the lanes of a wave (one read each, in every kernel that
+// touches the slots) access the same entry index at adjacent addresses.  Workspaces hold whole waves.
+inline int64_t intv_slot_at(int64_t li, int64_t k, int64_t cap) { return ((li >> 6) * cap + k) * 64 + (li & 63); }
+inline int64_t intv_slot_reads(int64_t n) { return (n + 63) / 64 * 64; }
+
+#ifdef __HIP__
+// A lane's array interleaved with the other lanes of its wave: element i at p[i * 64].
+template <typename T> struct SP {
+    T *p;
+    __host__ __device__ T &operator[](int i) const { return p[(size_t)i * 64]; }
+    __host__ __device__ SP operator+(int i) const { return SP{p + (size_t)i * 64}; }
+};
+__device__ inline int64_t intv_slot_at_d(int64_t li, int64_t k, int64_t cap) { return ((li >> 6) * cap + k) * 64 + (li & 63); }
+#endif
+
 // Device view of the index (passed by value as a kernel argument).
 struct DIndex {
     const OccBlock *occ;

@@ -251,8 +251,8 @@ struct LList {
     }
 };
 
-struct OutSlot {   // the read's output intervals (global), mem grows from the front, mem1 from the back
-    Intv *a;
+struct OutSlot {   // the read's output intervals (global, wave-interleaved), mem grows from the front, mem1 from the back
+    SP<Intv> a;
     int n, cap, n1;
 };
 
@@ -538,7 +538,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
         const uint8_t *q = codes + offs[li];
         const int len = (int)(offs[li + 1] - offs[li]);
         bool ovf = false;
-        OutSlot S{intv_out + (size_t)li * cp.intv, 0, cp.intv, 0};
+        OutSlot S{SP<Intv>{intv_out + intv_slot_at_d(li, 0, cp.intv)}, 0, cp.intv, 0};
         const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
         auto take_mem1 = [&](bool pass2) {
             // mem1 (reversed emission order) sits at S.a[cap-n1 .. cap); filter-append in order
@@ -584,7 +584,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             status[li] |= ST_OVERFLOW;
             n_intv[li] = 0;
         } else {
-            Intv *out = S.a;
+            const SP<Intv> out = S.a;
             for (int a = 1; a < S.n; ++a) {   // equal keys are identical intervals: any correct sort is exact
                 const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
                 int b = a;
