@@ -56,7 +56,7 @@ hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, cons
 hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
-                           Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int);
+                           Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
 struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
 struct RenderView {
@@ -677,6 +677,7 @@ struct Workspace {
     int zslab_blocks = 0;
     int32_t *dlist0 = nullptr, *dlist1 = nullptr, *dcount = nullptr;   // reads deferred by the group kernels
     uint8_t *lspill = nullptr;   // SMEM list entries beyond the LDS share (main pass), LSPILL per read
+    uint8_t *codes_t = nullptr;  // wave-transposed read codes for the main-pass seeding kernel (reads <= 1024 bases)
     uint32_t *ekey0 = nullptr, *ekey1 = nullptr;   // extension work keys (main pass) and their sort
     int32_t *eidx0 = nullptr, *eidx1 = nullptr;
     void *esort_tmp = nullptr;
@@ -688,7 +689,7 @@ struct Workspace {
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
         hipFree(sscore);
         hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
-        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill);
+        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill); hipFree(codes_t);
         *this = Workspace{};
     }
 };
@@ -752,6 +753,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
         HIPCHK(hipMalloc(&w.dcount, 16));
         HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 4)));
+        if (cp.max_len <= 1024) HIPCHK(hipMalloc(&w.codes_t, (size_t)intv_slot_reads((int64_t)R) * (size_t)cp.max_len));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
         HIPCHK(hipMalloc(&w.ekey1, R * 4));
         HIPCHK(hipMalloc(&w.eidx0, R * 4));
@@ -1060,7 +1062,7 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
         const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 8;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
-                               w.lspill, tiny_caps() ? 0 : LSPILL));
+                               w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
     } else {
         HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }

@@ -256,8 +256,8 @@ struct OutSlot {   // the read's output intervals (global, wave-interleaved), me
     int n, cap, n1;
 };
 
-template <typename X>
-DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_intv, LList<X> &L, OutSlot &S,
+template <typename X, typename Q>
+DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &L, OutSlot &S,
                   bool &ovf, uint64_t &nblk, uint64_t &nkm)
 {
     S.n1 = 0;
@@ -449,8 +449,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, const uint8_t *q, int x, int min_int
     return ret;
 }
 
-template <typename X>
-DEV int seed_strategy1_x(const FM<X> &fm, int len, const uint8_t *q, int x, int min_len, int max_intv, Intv &mem,
+template <typename X, typename Q>
+DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int max_intv, Intv &mem,
                          uint64_t &nblk, uint64_t &nkm)
 {
     mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
@@ -505,10 +505,30 @@ DEV void wave_add2(unsigned long long *dst, unsigned long long v)
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
 }
 
-template <typename X>
+// A read's bases in the wave-transposed copy (k_codes_wave): base i at p[i * 64], so the lanes of a wave
+// reading base i of their reads load one contiguous 64-B line instead of 64 lines.
+struct QT {
+    const uint8_t *p;
+    DEV int operator[](int i) const { return p[(size_t)i * 64]; }
+};
+
+// codes_t[(li / 64) * 64 * L + i * 64 + li % 64] = base i of read li (i < its length; L = the batch's
+// read-length cap).  One block per 64 reads; a thread copies every 4th base of one read.
+__global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const int64_t *offs, int n, int L,
+                                                    uint8_t *codes_t)
+{
+    const int lane = threadIdx.x & 63, li = blockIdx.x * 64 + lane;
+    if (li >= n) return;
+    const uint8_t *q = codes + offs[li];
+    const int len = (int)(offs[li + 1] - offs[li]);
+    uint8_t *d = codes_t + (size_t)blockIdx.x * 64 * (size_t)L + lane;
+    for (int i = (int)(threadIdx.x >> 6); i < len; i += 4) d[(size_t)i * 64] = q[i];
+}
+
+template <typename X, typename Q>
 __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
-                                                  Counters *ctr, int lcap, uint8_t *spill, int gcap)
+                                                  Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
 {
     const int T = blockDim.x, t = threadIdx.x;
     LList<X> L;
@@ -535,7 +555,9 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     uint64_t nblk = 0, nkm = 0;
     const int li = blockIdx.x * T + t;
     if (li < n) {
-        const uint8_t *q = codes + offs[li];
+        Q q;
+        if constexpr (__is_same(Q, QT)) q = QT{codes + (size_t)(li >> 6) * 64 * (size_t)qcap + (li & 63)};   // codes_t
+        else q = codes + offs[li];
         const int len = (int)(offs[li + 1] - offs[li]);
         bool ovf = false;
         OutSlot S{SP<Intv>{intv_out + intv_slot_at_d(li, 0, cp.intv)}, 0, cp.intv, 0};
@@ -607,23 +629,35 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
 template <typename X>
 static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (2 * sizeof(X) + 2); }
 
+// codes_t: a workspace buffer of ceil(n / 64) * 64 * cp.max_len bytes for the wave-transposed copy of the
+// reads (nullptr: the kernel reads the packed codes)
 hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                            const int64_t *offs, int n, Intv *intv, int32_t *n_intv, uint32_t *status, Counters *ctr,
-                           int lcap, uint8_t *spill, int gcap)
+                           int lcap, uint8_t *spill, int gcap, uint8_t *codes_t)
 {
     // one-wave blocks: a block's LDS lists are released when its wave ends, not when the slowest of four
     // waves does (C2 +2.7 %, C3 +1.4 % against 256-lane blocks at the same 16 waves per CU)
     const int T = 64;
     const int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
+    const int L = cp.max_len;
+    if (codes_t) hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), 0, st, codes, offs, n, L, codes_t);
     if (!ix.wide) {
         size_t sh = lds_bytes<uint32_t>(T, lcap);
-        hipLaunchKernelGGL(k_smem_lds<uint32_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap, spill, gcap);
+        if (codes_t)
+            hipLaunchKernelGGL((k_smem_lds<uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, intv,
+                               n_intv, status, ctr, lcap, spill, gcap, L);
+        else
+            hipLaunchKernelGGL((k_smem_lds<uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs,
+                               n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
     } else {
         size_t sh = lds_bytes<uint64_t>(T, lcap);
-        hipLaunchKernelGGL(k_smem_lds<uint64_t>, dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs, n, intv, n_intv,
-                           status, ctr, lcap, spill, gcap);
+        if (codes_t)
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, intv,
+                               n_intv, status, ctr, lcap, spill, gcap, L);
+        else
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs,
+                               n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
     }
     return hipGetLastError();
 }
