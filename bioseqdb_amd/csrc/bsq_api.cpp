@@ -1057,10 +1057,12 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     hipStream_t st = b->stream;
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
-        // 15 entries in LDS = 38.4 KB per 256-lane block: 4 blocks (16 waves) per CU; longer lists spill.
+        // u32 rows: 15 entries in LDS = 9.6 KB per one-wave block, 16 waves per CU; longer lists spill.
+        // 64-bit rows: the kernel's VGPRs allow 8 waves per CU, so 16 entries (18.4 KB) fit (C4 19.0 -> 21.8M
+        // reads/s against 8 entries).
         // BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested (tests/test_gpu_parity.py).
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 8;
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 16;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
     } else {
