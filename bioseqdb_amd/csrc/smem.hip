@@ -513,16 +513,21 @@ struct QT {
 };
 
 // codes_t[(li / 64) * 64 * L + i * 64 + li % 64] = base i of read li (i < its length; L = the batch's
-// read-length cap).  One block per 64 reads; a thread copies every 4th base of one read.
+// read-length cap).  One block per 64 reads: the wave's reads are contiguous in `codes`, so they are staged in
+// LDS with coalesced loads, then written out transposed (64 lanes store one 64-B line per base index).
+extern __shared__ uint8_t g_codes_stage[];
 __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const int64_t *offs, int n, int L,
                                                     uint8_t *codes_t)
 {
-    const int lane = threadIdx.x & 63, li = blockIdx.x * 64 + lane;
-    if (li >= n) return;
-    const uint8_t *q = codes + offs[li];
-    const int len = (int)(offs[li + 1] - offs[li]);
+    const int r0 = blockIdx.x * 64, r1 = r0 + 64 < n ? r0 + 64 : n;
+    const int64_t b0 = offs[r0], nb = offs[r1] - b0;   // <= 64 * L bytes
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) g_codes_stage[i] = codes[b0 + i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, li = r0 + lane;
+    if (li >= r1) return;
+    const int s = (int)(offs[li] - b0), len = (int)(offs[li + 1] - offs[li]);
     uint8_t *d = codes_t + (size_t)blockIdx.x * 64 * (size_t)L + lane;
-    for (int i = (int)(threadIdx.x >> 6); i < len; i += 4) d[(size_t)i * 64] = q[i];
+    for (int i = (int)(threadIdx.x >> 6); i < len; i += 4) d[(size_t)i * 64] = g_codes_stage[s + i];
 }
 
 template <typename X, typename Q>
@@ -641,7 +646,8 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
     const int L = cp.max_len;
-    if (codes_t) hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), 0, st, codes, offs, n, L, codes_t);
+    if (codes_t)
+        hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
     if (!ix.wide) {
         size_t sh = lds_bytes<uint32_t>(T, lcap);
         if (codes_t)
