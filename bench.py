@@ -45,12 +45,16 @@ STAGE_KERNEL = {"smem": "k_codes_wave+k_smem_lds", "chain": "k_chain", "extend":
                 "reg2aln": "k_r2a_key+sort+k_reg2aln_g16+g32+w"}
 # per-launch HBM traffic from the committed PMC passes (tools/profile_round.sh + tools/traffic_from_pmc.py,
 # FETCH_SIZE corrected by the calib_fetch.hip gather calibration); PMC cannot be collected in-process
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+TRAFFIC_JSON = {"c3": os.path.join(ROOT, "profiles", "traffic.json"),
+                "c2": os.path.join(ROOT, "profiles", "traffic_c2.json"),
+                "c4": os.path.join(ROOT, "profiles", "traffic_c4.json")}
 
 
-def traffic_for(stage: str, reads: int):
+def traffic_for(stage: str, reads: int, config: str = "c3"):
+    """PMC traffic of `stage` scaled to a launch of `reads` reads (the committed per-launch figure of the
+    profiled lone launches), and the profile round it comes from."""
     try:
-        t = json.load(open(TRAFFIC_JSON))
+        t = json.load(open(TRAFFIC_JSON[config]))
         k = t["kernels"][stage]
         return k["traffic_bytes"] * reads / t["reads_per_launch"], t["round"]
     except (OSError, KeyError, ValueError):
@@ -242,6 +246,242 @@ def reads_as_nuclseq(L, reads):
     return keep, ptrs
 
 
+def lone_launch(L, idx, opts, codes, offs, n, first_call):
+    """Every stage of the path as one lone launch over n reads (one batch, nothing else on the GPU), after a
+    warm-up run: per-stage HIP-event ms and issued bytes on the batch stream."""
+    wb = ctypes.c_void_p()
+    N.check(L.bsq_batch_create(idx, n, int(offs[n] - offs[0]), ctypes.byref(wb)))
+    try:
+        N.check(L.bsq_batch_set_reads(wb, codes.ctypes.data, offs.ctypes.data, n))
+        for _ in range(2):   # warm-up + measured
+            N.check(L.bsq_batch_run(wb, ctypes.byref(opts), first_call))
+        ms = (ctypes.c_float * 6)()
+        L.bsq_batch_stage_ms(wb, ms, 6)
+        by = (ctypes.c_double * 6)()
+        L.bsq_batch_stage_bytes(wb, by, 6)
+        return [float(x) for x in ms], [float(x) for x in by]
+    finally:
+        L.bsq_batch_free(wb)
+
+
+def oracle_index(L, idx, ref_ns):
+    """The CPU oracle's index over the same reference rows, its FM tables from the device-built suffix array
+    (the checker for parity and the CPU baseline; test infrastructure, never on the product path)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    oi = O.OracleIndex()
+    for buf in ref_ns:
+        oi.add_ref(len(oi._keep) + 1, bytes(buf.raw))
+    eb = ctypes.c_int()
+    N.check(L.bsq_index_download(idx))   # host copy of the SA for the oracle's index
+    sa = L.bsq_index_sa_data(idx, ctypes.byref(eb))
+    oi.build_from_sa(sa, eb.value)
+    return O, oi
+
+
+def cpu_baseline(O, oi, oo, codes, offs, n_reads, threads, seeding, seconds, first_call):
+    """The oracle timed on this host: a warm-up that sizes the sample, then the median of 3 runs
+    on `threads` threads (~seconds/3 each) and the median of 3 single-thread runs (~seconds/6 each)."""
+    def run(n, th):
+        ck = ctypes.c_uint64()
+        t = time.perf_counter()
+        if seeding:
+            nreg = O.lib().orc_seed_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, th,
+                                          ctypes.byref(ck))
+        else:
+            nreg = O.lib().orc_align_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, first_call,
+                                           th, ctypes.byref(ck))
+        return time.perf_counter() - t, nreg, ck.value
+
+    n0 = min(2000, n_reads)
+    dt, _, _ = run(n0, threads)
+    sample = int(min(n_reads, max(n0, n0 / max(dt, 1e-6) * seconds / 3)))
+    times = []
+    for _ in range(3):
+        dt, nreg, ck = run(sample, threads)
+        times.append(dt)
+    ab = (ctypes.c_uint64 * 4)()
+    O.lib().orc_algo_bytes(ab)   # SURVEY.md 8(d) bytes of the sample, counted on libbwa's layout
+    m0 = min(300, n_reads)
+    dt, _, _ = run(m0, 1)
+    n1 = int(min(n_reads, max(m0, m0 / max(dt, 1e-6) * seconds / 6)))
+    times1 = [run(n1, 1)[0] for _ in range(3)]
+    med, med1 = sorted(times)[1], sorted(times1)[1]
+    return {"sample": sample, "times": times, "nreg": nreg, "ck": ck, "ab": list(ab), "n1": n1, "times1": times1,
+            "value": round(sample / med, 1), "value_1thread": round(n1 / med1, 1)}
+
+
+def make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, iso_reads, per_read, tr, S):
+    """The bench line's `roofline` for the dominant stage: the lone launch over all the step's reads when there
+    is one (the kernel's own time), with the shared-CU figure of the timed concurrent batches beside it.
+    `achieved` = SURVEY.md 8(d) algorithmic bytes per launch (oracle-counted per read x reads) / launch time."""
+    def fig(ms, issued, n):
+        d = {"reads_per_launch": int(round(n)), "launch_ms": round(ms, 3), "issued_bytes_per_launch": issued,
+             "issued_gbs": round(issued / (ms * 1e-3) / 1e9, 2) if ms > 0 else 0.0}
+        alg = per_read[di] * n if per_read else issued
+        d["algorithmic_bytes_per_launch"] = alg
+        d["achieved"] = round(alg / (ms * 1e-3) / 1e9, 2) if ms > 0 else 0.0
+        d["frac"] = round(d["achieved"] / HBM_PEAK_GBS, 5)
+        return d
+    conc = fig(float(stage_ms[di]), float(stage_bytes[di]), reads_per_launch)
+    head = fig(float(iso[0][di]), float(iso[1][di]), iso_reads) if iso else conc
+    t, t_round = tr(dom, head["reads_per_launch"])
+    roof = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s", **head,
+            "traffic": t,
+            "traffic_source": (f"{t_round} rocprofv3 PMC FETCH_SIZE + WRITE_SIZE passes of lone launches, per launch"
+                               if t else "not measured for this shape"),
+            "basis": ("lone launch: one batch of all the step's reads with nothing else on the GPU (HIP events on the "
+                      "batch stream)" if iso else f"{S} concurrent batches (no lone launch in this run)"),
+            "bytes": "SURVEY.md 8(d) algorithmic bytes" if per_read else "bytes the kernels issue (no oracle sample)"}
+    if iso and S > 1:
+        roof["concurrent"] = dict(conc, note=f"{S} concurrent batches of the timed step: the kernel's duration while it "
+                                             "shares the CUs with the other batches' stages")
+    return roof
+
+
+def run_group(args, cfg) -> int:
+    """--gpus N from one process (no launcher): the devices driven the way a Postgres backend drives them
+    (bsq_group): the index built once on the first device and broadcast over RCCL, member k
+    aligning its own reads (seed READ_SEED + k, weak scaling) as concurrent shares on its device, each member's
+    records copied to pinned host memory over its own PCIe link.  One step = one bsq_group_run over the
+    members' reads already staged on their devices; it ends when every record is in host memory (segments in
+    read order).  The merged single view is timed separately (`merge_ms`)."""
+    L = N.lib()
+    G = args.gpus if not args.group_devices else len(args.group_devices.split(","))
+    devs = [int(x) for x in args.group_devices.split(",")] if args.group_devices else list(range(G))
+    if args.gpus > 1 and len(devs) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but --group-devices lists {len(devs)} members")
+    ndev = L.bsq_device_count()
+    if ndev < max(devs) + 1:
+        raise SystemExit(f"--gpus {G}: {ndev} HIP device(s) visible, devices {devs} requested")
+    if cfg["seeding"]:
+        raise SystemExit("the device group runs the full path (configs c3/c4)")
+    hb = Heartbeat("bench group")
+    hb.phase = "generating the reference and reads"
+    ref = synth.make_reference(args.ref_bp, n_rows=cfg["rows"])
+    member_reads = [synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + k + args.seed_offset)
+                    for k in range(G)]
+    idx = ctypes.c_void_p()
+    N.check(L.bsq_index_create(ctypes.byref(idx)))
+    ref_ns = []
+    for i, t in enumerate(ref.texts()):
+        size = ctypes.c_size_t()
+        p = L.bsq_nuclseq_from_text(t, len(t), ctypes.byref(size))
+        buf = ctypes.create_string_buffer(ctypes.string_at(p, size.value), size.value)
+        L.bsq_free(p)
+        ref_ns.append(buf)
+        N.check(L.bsq_index_add_ref(idx, i + 1, ctypes.addressof(buf)))
+    hb.phase = "building the index on the first member's GPU"
+    t0 = time.time()
+    N.check(L.bsq_index_build_device(idx, devs[0]))
+    t_build = time.time() - t0
+    opts = default_opts(int(L.bsq_index_n_refs(idx)))
+    g = ctypes.c_void_p()
+    darr = (ctypes.c_int * G)(*devs)
+    N.check(L.bsq_group_create(darr, G, ctypes.byref(g)))
+    N.check(L.bsq_group_set_slots(g, max(1, args.streams)))
+    hb.phase = "replicating the index over the group"
+    bc_ms = ctypes.c_double()
+    N.check(L.bsq_group_replicate(g, idx, ctypes.byref(bc_ms)))
+    # the members' reads as one cursor batch of nuclseq varlenas (member k: reads [k*n, (k+1)*n))
+    keep, n_tot = [], G * args.reads
+    ptrs = (ctypes.c_void_p * n_tot)()
+    for k, r in enumerate(member_reads):
+        kk, pk = reads_as_nuclseq(L, r)
+        keep += [kk, pk]
+        ctypes.memmove(ctypes.addressof(ptrs) + k * args.reads * ctypes.sizeof(ctypes.c_void_p), pk,
+                       args.reads * ctypes.sizeof(ctypes.c_void_p))
+    first_call = args.seed_offset * args.reads
+    hb.phase = "aligning"
+    N.check(L.bsq_group_run(g, ctypes.byref(opts), ptrs, n_tot, first_call))   # stages every member's reads
+    for _ in range(max(args.warmup - 1, 0)):
+        N.check(L.bsq_group_run(g, ctypes.byref(opts), None, n_tot, first_call))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        N.check(L.bsq_group_run(g, ctypes.byref(opts), None, n_tot, first_call))
+    elapsed = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    H = L.bsq_group_hits(g)
+    merge_ms = (time.perf_counter() - t1) * 1e3
+    if not H:
+        raise N.BsqError(N.BSQ_E_NOMEM, L.bsq_last_error().decode())
+    H = H.contents
+    value = n_tot * args.steps / elapsed
+    segs = (ctypes.POINTER(N.Hits) * 1024)()
+    slo = (ctypes.c_int32 * 1024)()
+    n_seg = L.bsq_group_segments(g, segs, slo, 1024)
+    result = {
+        "metric": cfg["metric"], "value": round(value, 1), "unit": "reads/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {
+            "workload": cfg["label"], "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
+            "parallelism": f"read-sharded x{G} in one process (bsq_group: index broadcast over RCCL, each member's "
+                           "records to host memory over its own PCIe link)",
+            "devices": devs, "distinct_devices": len(set(devs)), "shares_per_member": max(1, args.streams),
+            "segments": n_seg, "hits_per_step": int(H.n_hits),
+        },
+        "exchange": {"path": "per-member pinned D2H inside the step (segments in read order); merged view after it",
+                     "merge_ms": round(merge_ms, 3), "broadcast_ms": round(bc_ms.value, 2)},
+        "index_build_s": round(t_build, 2),
+    }
+    if args.checksums:   # member k's rows with member-local read indices (= a one-GPU run with --seed-offset k)
+        cks = [0] * G
+        for i in range(n_seg):
+            k = slo[i] // args.reads
+            v = segs[i].contents
+            cks[k] += gpu_checksum_vec(v, int(v.n_reads), slo[i] - k * args.reads)
+        result["checksums"] = [c & 0xFFFFFFFFFFFFFFFF for c in cks]
+    # parity of the first and the last member against the CPU oracle on a sample of their reads, and SURVEY.md
+    # 8(d)'s per-read bytes counted on it (a check, not a CPU baseline: that is the N = 1 line's)
+    per_read = None
+    if not args.no_cpu_baseline:
+        hb.phase = "oracle parity sample"
+        O, oi = oracle_index(L, idx, ref_ns)
+        oo = O.opts_from(opts)
+        th = host_cpus()["usable"]
+        par = []
+        for k in sorted({0, G - 1}):
+            r = member_reads[k]
+            m = min(2000, r.n)
+            c_ = np.ascontiguousarray(r.codes)
+            o_ = np.ascontiguousarray(r.offsets)
+            ck = ctypes.c_uint64()
+            O.lib().orc_align_batch(oi.h, ctypes.byref(oo), c_.ctypes.data, o_.ctypes.data, m,
+                                    first_call + k * args.reads, th, ctypes.byref(ck))
+            if k == 0:
+                ab = (ctypes.c_uint64 * 4)()
+                O.lib().orc_algo_bytes(ab)
+                per_read = [ab[0] / m + (args.read_len + 3) // 4, ab[1] / m, ab[2] / m, ab[3] / m]
+            gck = 0
+            for i in range(n_seg):
+                loc = slo[i] - k * args.reads   # segment start within member k
+                if slo[i] // args.reads != k or loc >= m:
+                    continue
+                v = segs[i].contents
+                gck += gpu_checksum_vec(v, min(int(v.n_reads), m - loc), loc)
+            par.append({"member": k, "reads": m, "checksum_match": (gck & 0xFFFFFFFFFFFFFFFF) == ck.value})
+        result["parity_sample"] = par
+    # roofline of the dominant stage: member 0's reads as one lone launch on its device
+    hb.phase = "isolated single-batch launch"
+    r0 = member_reads[0]
+    codes = np.ascontiguousarray(r0.codes)
+    offs = np.ascontiguousarray(r0.offsets)
+    names = [L.bsq_stage_name(i).decode() for i in range(6)]
+    iso = None if args.no_isolated else lone_launch(L, idx, opts, codes, offs, r0.n, first_call)
+    if iso:
+        di = max(range(4), key=lambda i: iso[0][i])
+        tr = (lambda stage, n: traffic_for(stage, n, args.config)) if (args.reads == cfg["reads"] and args.ref_bp == cfg["ref_bp"]) \
+            else (lambda stage, n: (None, None))
+        result["roofline"] = make_roofline(names[di], di, iso[0], iso[1], r0.n, iso, r0.n, per_read, tr, 1)
+        result["kernels"] = {STAGE_KERNEL[names[i]]: {"lone_ms": round(iso[0][i], 3)} for i in range(4)}
+    hb.stop()
+    print(json.dumps(result), flush=True)
+    L.bsq_group_free(g)
+    L.bsq_index_free(idx)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -269,6 +509,14 @@ def main() -> int:
                     help="run the N > 1 exchange path with a process group of one rank (tests it on a one-GPU box)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 exchange backend (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
+    ap.add_argument("--group-devices", default=None,
+                    help="in-process group (--gpus N without torchrun): comma-separated device of each member "
+                         "(default 0..N-1; a repeated device makes replicas on one GPU, for tests)")
+    ap.add_argument("--seed-offset", type=int, default=0,
+                    help="rank (or member) k aligns the reads of seed READ_SEED + k + offset, lrand48 position "
+                         "(k + offset) * reads: lets a one-GPU run reproduce any member of a multi-GPU run")
+    ap.add_argument("--checksums", action="store_true",
+                    help="add the oracle-format checksum of every rank/member's full read set to the line")
     args = ap.parse_args()
     if args.timed_only:
         args.no_cpu_baseline = args.no_codec = args.no_isolated = True
@@ -280,6 +528,11 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and (args.gpus > 1 or args.group_devices) and not args.exchange_world1:
+        # N GPUs from one process, the way a Postgres backend drives them (bsq_group): no torchrun needed
+        return run_group(args, cfg)
+    if world > 1 and args.gpus not in (1, world):
+        raise SystemExit(f"--gpus {args.gpus} under a launcher with WORLD_SIZE={world}: one rank per GPU expected")
     dist = None
     gpu = local
     xdev = None   # device of the exchange tensors
@@ -300,7 +553,7 @@ def main() -> int:
     hb.phase = "generating the reference and reads"
     t0 = time.time()
     ref = synth.make_reference(args.ref_bp, n_rows=cfg["rows"])
-    reads = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + rank)
+    reads = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + rank + args.seed_offset)
     t_gen = time.time() - t0
 
     # ---- index: built once (host, the step before the hot path), then in HBM on every GPU ----
@@ -355,7 +608,8 @@ def main() -> int:
     batch = batches[0]
     codes = np.ascontiguousarray(reads.codes)     # the whole batch, for the CPU baseline
     offs = np.ascontiguousarray(reads.offsets)
-    first_call = rank * reads.n   # lrand48 stream position as one backend aligning all ranks' reads in order
+    # lrand48 stream position as one backend aligning all ranks' reads in order
+    first_call = (rank + args.seed_offset) * reads.n
     b_arr = (ctypes.c_void_p * S)(*[b.value for b in batches])
     fc_arr = (ctypes.c_uint64 * S)(*[first_call + lo_k[k] for k in range(S)])
     log(f"[bench r{rank}] gen {t_gen:.1f}s index build {t_build:.1f}s upload {t_upload:.2f}s "
@@ -441,32 +695,22 @@ def main() -> int:
     n_hits = sum(int(L.bsq_batch_hits(b).contents.n_hits) for b in batches) if not cfg["seeding"] else 0
     retried = sum(int(L.bsq_batch_retried(b)) for b in batches)
     names = [L.bsq_stage_name(i).decode() for i in range(6)]
-    kern = {names[i]: float(stage_ms[i]) for i in range(1 if cfg["seeding"] else 4)}
-    # measured PMC traffic exists for the default C3 shape only (profiles/traffic.json)
-    tr = (lambda stage: traffic_for(stage, reads_per_launch)) if (args.config == "c3" and default_shape) else \
-        (lambda stage: (None, None))
+    nst = 1 if cfg["seeding"] else 4
+    kern = {names[i]: float(stage_ms[i]) for i in range(nst)}
+    # measured PMC traffic of lone launches (profiles/traffic*.json) exists for the default config shapes
+    tr = (lambda stage, n: traffic_for(stage, n, args.config)) if default_shape else (lambda stage, n: (None, None))
     dom = max(kern, key=kern.get)
     di = names.index(dom)
-    achieved = stage_bytes[di] / (stage_ms[di] * 1e-3) / 1e9 if stage_ms[di] > 0 else 0.0
 
-    # the dominant stage once more as a lone launch over all the reads (one batch, nothing sharing the CUs),
-    # outside the timed region: the kernel's own roofline beside the shared-CU figure of the timed run
+    # the stages once more as one lone launch over all the reads (one batch, nothing sharing the CUs), outside
+    # the timed region: each kernel's own roofline (the headline `roofline`), beside the shared-CU figures of
+    # the timed concurrent batches.  With one batch per step the timed launches are lone launches already.
     iso = None
     if world == 1 and S > 1 and not cfg["seeding"] and not args.no_isolated:
         hb.phase = "isolated single-batch launch"
-        wb = ctypes.c_void_p()
-        N.check(L.bsq_batch_create(idx, reads.n, int(reads.offsets[-1]), ctypes.byref(wb)))
-        try:
-            N.check(L.bsq_batch_set_reads(wb, codes.ctypes.data, offs.ctypes.data, reads.n))
-            for _ in range(2):   # warm-up + measured
-                N.check(L.bsq_batch_run(wb, ctypes.byref(opts), first_call))
-            ms = (ctypes.c_float * 6)()
-            L.bsq_batch_stage_ms(wb, ms, 6)
-            by = (ctypes.c_double * 6)()
-            L.bsq_batch_stage_bytes(wb, by, 6)
-            iso = (float(ms[di]), float(by[di]))
-        finally:
-            L.bsq_batch_free(wb)
+        iso = lone_launch(L, idx, opts, codes, offs, reads.n, first_call)
+    elif S == 1:
+        iso = (list(stage_ms), list(stage_bytes))
 
     total_reads = args.reads * world
     value = total_reads * args.steps / elapsed
@@ -486,41 +730,38 @@ def main() -> int:
         "config": {
             "workload": cfg["label"],
             "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
-            "parallelism": f"read-sharded x{world}", "hits_per_step_rank0": n_hits,
-            "streams": S, "reads_per_launch": int(round(reads_per_launch)),
+            "parallelism": f"read-sharded x{world}" + (" (one process per GPU, RCCL record gather)" if world > 1 else ""),
+            "hits_per_step_rank0": n_hits, "streams": S, "reads_per_launch": int(round(reads_per_launch)),
         },
         "exchange": None if xchg is None else {
             "path": ("RCCL gather of device records to rank 0, pinned D2H there, overlapped with the next step"
                      if xchg.gpu else "gloo gather of host records to rank 0 (rehearsal)"),
             "bytes_per_step_rank0": int(xchg.bytes_moved / max(args.steps + args.warmup, 1)) if rank == 0 else None,
         },
-        "roofline": {
-            "bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": tr(dom)[0],
-            "traffic_source": (f"profiles/traffic.json ({tr(dom)[1]} PMC FETCH_SIZE+WRITE_SIZE per launch)"
-                               if tr(dom)[0] else "not measured for this shape"),
-            "algorithmic_bytes_per_launch": float(stage_bytes[di]), "launch_ms": round(float(stage_ms[di]), 3),
-            "launches": (f"{S} concurrent batches of {int(round(reads_per_launch))} reads; launch_ms is the kernel's "
-                         "duration while it shares the CUs with the other batches' stages" if S > 1 else "one batch"),
-        },
         "kernels": {
             STAGE_KERNEL[nm]: {
-                "ms": round(float(stage_ms[i]), 3), "algorithmic_bytes": float(stage_bytes[i]),
-                "achieved_gbs": round(stage_bytes[i] / (stage_ms[i] * 1e-3) / 1e9, 2) if stage_ms[i] > 0 else 0.0,
-                "traffic_bytes": tr(nm)[0],
+                "ms": round(float(stage_ms[i]), 3), "issued_bytes": float(stage_bytes[i]),
+                "issued_gbs": round(stage_bytes[i] / (stage_ms[i] * 1e-3) / 1e9, 2) if stage_ms[i] > 0 else 0.0,
+                "lone_ms": round(float(iso[0][i]), 3) if iso else None,
+                "lone_traffic_bytes": tr(nm, reads.n)[0],
+                "lone_traffic_gbs": (round(tr(nm, reads.n)[0] / (iso[0][i] * 1e-3) / 1e9, 2)
+                                     if iso and tr(nm, reads.n)[0] and iso[0][i] > 0 else None),
                 "work": float(stage_work[i]),
-                "traffic_gbs": (round(tr(nm)[0] / (stage_ms[i] * 1e-3) / 1e9, 2)
-                                if tr(nm)[0] and stage_ms[i] > 0 else None),
-            } for i, nm in enumerate(names[:1 if cfg["seeding"] else 4])
+            } for i, nm in enumerate(names[:nst])
         },
         "stages_ms": {names[i]: round(float(stage_ms[i]), 3) for i in range(6)},
-        "stages_algorithmic_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
+        "stages_issued_bytes": {names[i]: float(stage_bytes[i]) for i in range(6)},
         "stages_work": {names[i]: float(stage_work[i]) for i in range(6)},
         "index_build_s": round(t_build, 2),
         "index_build": args.index_build,
         "index_upload_s": round(t_upload, 2),
         "retried_reads": retried,
     }
+    if args.checksums and not cfg["seeding"]:
+        ck = 0
+        for k, b in enumerate(batches):
+            ck += gpu_checksum_vec(L.bsq_batch_hits(b).contents, lo_k[k + 1] - lo_k[k], lo_k[k])
+        result["checksums"] = [ck & 0xFFFFFFFFFFFFFFFF]
 
     # ---- host materialisation: the last step's rows rendered as bwa_result text ----
     if rank == 0 and not cfg["seeding"] and n_hits and not args.timed_only:
@@ -640,40 +881,15 @@ def main() -> int:
         del raw, vals, tcat
 
     # ---- CPU baseline: the oracle on this host, bounded sample, rank 0 at N = 1 only ----
-    hb.phase = "CPU baseline"
+    per_read = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_py as O
-        oi = O.OracleIndex()
-        for buf in ref_ns:
-            oi.add_ref(len(oi._keep) + 1, bytes(buf.raw))
-        eb = ctypes.c_int()
-        N.check(L.bsq_index_download(idx))   # host copy of the SA for the oracle's index
-        sa = L.bsq_index_sa_data(idx, ctypes.byref(eb))
-        oi.build_from_sa(sa, eb.value)
+        hb.phase = "CPU baseline"
+        O, oi = oracle_index(L, idx, ref_ns)
         oo = O.opts_from(opts)
         host = host_cpus()
         threads = args.cpu_threads or host["usable"]
-
-        def run_cpu(n, th):
-            ck = ctypes.c_uint64()
-            t = time.perf_counter()
-            if cfg["seeding"]:
-                nreg = O.lib().orc_seed_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, th,
-                                              ctypes.byref(ck))
-            else:
-                nreg = O.lib().orc_align_batch(oi.h, ctypes.byref(oo), codes.ctypes.data, offs.ctypes.data, n, 0, th,
-                                               ctypes.byref(ck))
-            return time.perf_counter() - t, nreg, ck.value
-
-        dt, _, _ = run_cpu(min(2000, reads.n), threads)            # calibration / warm-up
-        rate = min(2000, reads.n) / max(dt, 1e-6)
-        sample = int(min(reads.n, max(2000, rate * args.cpu_seconds)))
-        dt, nreg, ck = run_cpu(sample, threads)
-        ab = (ctypes.c_uint64 * 4)()
-        O.lib().orc_algo_bytes(ab)   # SURVEY.md 8(d) bytes of the sample, counted on libbwa's layout
-        n1 = min(2000, reads.n)       # the single-backend rate (the reference's SQL path is one thread)
-        dt1, _, _ = run_cpu(n1, 1)
+        cb = cpu_baseline(O, oi, oo, codes, offs, reads.n, threads, cfg["seeding"], args.cpu_seconds, first_call)
+        sample = cb["sample"]
         if cfg["seeding"]:
             ro = ctypes.POINTER(ctypes.c_int64)()
             ivp = ctypes.POINTER(ctypes.c_uint64)()
@@ -690,47 +906,33 @@ def main() -> int:
                     gck += gpu_checksum_vec(L.bsq_batch_hits(b).contents, m, lo_k[k])
             gck &= 0xFFFFFFFFFFFFFFFF
         result["cpu_baseline"] = {
-            "value": round(sample / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample} reads of the same batch, CPU oracle (oracle/bwa_oracle.c, -O2), "
-                      f"{threads} threads = every core this process may use; 1-thread rate "
-                      f"{round(n1 / dt1, 1)} reads/s on {n1} reads",
-            "value_1thread": round(n1 / dt1, 1),
+            "value": cb["value"], "unit": "reads/s", "cores": threads, "kind": "port",
+            "sample": (f"first {sample} reads of the same batch, CPU oracle (oracle/bwa_oracle.c, -O2), {threads} threads "
+                       f"= every core this process may use; median of 3 runs after a warm-up "
+                       f"(runs {', '.join(f'{t:.2f}' for t in cb['times'])} s); 1 thread: median of 3 over "
+                       f"{cb['n1']} reads ({', '.join(f'{t:.2f}' for t in cb['times1'])} s)"),
+            "value_1thread": cb["value_1thread"],
             "host": host,
         }
-        result["parity_sample"] = {"reads": sample, ("intervals" if cfg["seeding"] else "regions"): int(nreg),
-                                   "checksum_match": bool(gck == ck)}
-        result["gpu_vs_cpu"] = round(value / (sample / dt), 1)
-        # roofline `achieved` per the contract: SURVEY.md 8(d)'s per-read algorithmic bytes (libbwa's own
-        # layout, counted by the oracle on this sample) x the reads of one launch / the launch time.  The
-        # bytes the kernels issue from this repo's layout (k-mer table, 64-base rank blocks, full SA) stay
-        # beside it as `issued`.
+        result["parity_sample"] = {"reads": sample, ("intervals" if cfg["seeding"] else "regions"): int(cb["nreg"]),
+                                   "checksum_match": bool(gck == cb["ck"])}
+        result["gpu_vs_cpu"] = round(value / cb["value"], 1)
+        result["gpu_vs_cpu_1thread"] = round(value / cb["value_1thread"], 1)
+        # SURVEY.md 8(d)'s per-read algorithmic bytes (libbwa's own layout, counted by the oracle on this sample)
         reads_bytes_per_read = (args.read_len + 3) // 4   # the packed read (2 bits per base)
+        ab = cb["ab"]
         per_read = [ab[0] / sample + reads_bytes_per_read, ab[1] / sample, ab[2] / sample, ab[3] / sample]
-        rf = result["roofline"]
-        ki = names.index(dom)
-        if ki < (1 if cfg["seeding"] else 4):
-            alg = per_read[ki] * reads_per_launch
-            rf["issued_bytes_per_launch"] = rf.pop("algorithmic_bytes_per_launch")
-            rf["issued_gbs"] = rf["achieved"]
-            rf["frac_issued"] = rf["frac"]
-            rf["algorithmic_bytes_per_launch"] = alg
-            rf["algorithmic_bytes_per_read"] = round(per_read[ki], 1)
-            rf["algorithmic_source"] = (f"SURVEY.md 8(d): oracle-counted on libbwa's layout over the {sample}-read "
-                                        "sample (64 B per occ block of bwt_extend, 8 B per SA value, ceil(bases/4) "
-                                        "per reference window, + the packed read)")
-            rf["achieved"] = round(alg / (rf["launch_ms"] * 1e-3) / 1e9, 2)
-            rf["frac"] = round(rf["achieved"] / HBM_PEAK_GBS, 5)
-            if iso:
-                a_iso = per_read[ki] * reads.n / (iso[0] * 1e-3) / 1e9
-                rf["isolated"] = {"reads_per_launch": reads.n, "launch_ms": round(iso[0], 3),
-                                  "achieved": round(a_iso, 2), "frac": round(a_iso / HBM_PEAK_GBS, 5),
-                                  "issued_gbs": round(iso[1] / (iso[0] * 1e-3) / 1e9, 2),
-                                  "note": "one untimed launch over all reads with nothing else on the GPU"}
-        for i, nm in enumerate(names[:1 if cfg["seeding"] else 4]):
+        for i, nm in enumerate(names[:nst]):
             k = result["kernels"][STAGE_KERNEL[nm]]
-            k["algorithmic_bytes_8d"] = per_read[i] * reads_per_launch
+            k["algorithmic_bytes_8d_per_read"] = round(per_read[i], 1)
             k["achieved_gbs_8d"] = (round(per_read[i] * reads_per_launch / (k["ms"] * 1e-3) / 1e9, 2)
                                     if k["ms"] > 0 else 0.0)
+            if iso and iso[0][i] > 0:
+                k["lone_achieved_gbs_8d"] = round(per_read[i] * reads.n / (iso[0][i] * 1e-3) / 1e9, 2)
+        result["roofline_source"] = (f"SURVEY.md 8(d) bytes: oracle-counted on libbwa's layout over the {sample}-read "
+                                     "sample (64 B per occ block of bwt_extend, 8 B per SA value, ceil(bases/4) per "
+                                     "reference window, + the packed read)")
+    result["roofline"] = make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, reads.n, per_read, tr, S)
     hb.stop()
     if rank == 0:
         print(json.dumps(result), flush=True)

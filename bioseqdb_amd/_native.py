@@ -130,6 +130,16 @@ SIGNATURES = {
     "bsq_group_run": (ctypes.c_int, [_P, ctypes.POINTER(Opts), _P, ctypes.c_int32, ctypes.c_uint64]),
     "bsq_group_hits": (ctypes.POINTER(Hits), [_P]),
     "bsq_group_render_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "bsq_group_set_slots": (ctypes.c_int, [_P, ctypes.c_int]),
+    "bsq_group_segments": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(Hits)), ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.c_int]),
+    "bsq_pipeline_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P)]),
+    "bsq_pipeline_free": (None, [_P]),
+    "bsq_pipeline_slots": (ctypes.c_int, [_P]),
+    "bsq_pipeline_submit": (ctypes.c_int, [_P, ctypes.POINTER(Opts), _P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int]),
+    "bsq_pipeline_next": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(Hits)), ctypes.POINTER(_P),
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))]),
+    "bsq_pipeline_release": (ctypes.c_int, [_P]),
 }
 
 _lib = None

@@ -24,6 +24,7 @@
 #include "../../include/bsq.h"
 #include "bsq_device.h"
 #include "bsq_index.h"
+#include "bsq_internal.h"
 
 namespace bsq {
 hipError_t launch_smem(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
@@ -180,7 +181,7 @@ extern "C" int bsq_index_create(bsq_index **out)
 extern "C" void bsq_index_free(bsq_index *idx)
 {
     if (!idx) return;
-    bsq_batch_free(idx->pool);
+    bsq_pipeline_free(idx->pipe);
     delete idx->h.dev;
     delete idx;
 }
@@ -794,7 +795,7 @@ struct bsq_batch {
     std::vector<int64_t> h_offs;
     std::vector<uint8_t> h_codes;   // staging copy of set_reads' codes
     // bsq_batch_set_nuclseqs: packed varlenas and their offsets on the device (grown on demand)
-    std::vector<uint8_t> ns_host;
+    NsStage stage;                  // host staging of bsq_batch_set_nuclseqs
     uint8_t *ns_dev = nullptr;
     int64_t ns_dev_cap = 0;
     int64_t *ns_meta = nullptr;   // in_off | poff | holed texts
@@ -1000,52 +1001,90 @@ static int grow_dev(T *&p, int64_t &cap, int64_t need);
 
 // Reads given as nuclseq varlenas (the cursor's detoasted values): the varlenas are
 // packed and uploaded as they are and turned into nt4 codes on the device (codec_gpu.hip, the same
-// pass as nuclseq_out with hole bases as code 4), instead of a per-read host conversion.
+// pass as nuclseq_out with hole bases as code 4), instead of a per-read host conversion.  The host half
+// (stage_nuclseqs) and the device half (batch_upload_staged) are separate so a pipeline can release a fetch's
+// tuples as soon as it is staged and upload it later from a worker thread (pipeline.cpp).
+namespace bsq {
+
+NsStage::~NsStage() { if (host) hipHostFree(host); }
+
+void set_error(const std::string &msg) { g_err = msg; }
+int32_t batch_max_reads(const bsq_batch *b) { return b->max_reads; }
+int64_t batch_max_bases(const bsq_batch *b) { return b->max_bases; }
+
+int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
+{
+    if (n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    const size_t n = (size_t)n_reads;
+    s.meta.assign(2 * (n + 1), 0);   // in_off | poff, then the holed reads
+    s.offs.assign(n + 1, 0);
+    int max_len = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
+        if (!ns) { set_err("read %zu is NULL", i); return BSQ_E_INVALID; }
+        uint32_t vl; memcpy(&vl, ns, 4);
+        const uint64_t nh = ns_holes_num(ns), len = ns_len(ns), need = 12 + 16 * nh + pac_byte_size(len);
+        if ((vl >> 2) < need) { set_err("read %zu: varlena of %u bytes, %llu needed", i, vl >> 2, (unsigned long long)need); return BSQ_E_INVALID; }
+        if (nh) s.meta.push_back((int64_t)i);
+        int64_t *in_off = s.meta.data(), *poff = s.meta.data() + n + 1;
+        in_off[i + 1] = in_off[i] + (int64_t)((need + 7) & ~7ull);
+        poff[i + 1] = poff[i] + (int64_t)pac_byte_size(len);
+        s.offs[i + 1] = s.offs[i] + (int64_t)len;
+        max_len = std::max<int>(max_len, (int)len);
+    }
+    const int64_t *in_off = s.meta.data(), *poff = s.meta.data() + n + 1;
+    const int64_t bytes = in_off[n];
+    if (bytes > s.host_cap) {
+        if (s.host) hipHostFree(s.host);
+        s.host = nullptr;
+        s.host_cap = 0;
+        const int64_t cap = std::max<int64_t>(bytes, 4096);
+        if (hipHostMalloc((void **)&s.host, (size_t)cap) != hipSuccess) { s.host = nullptr; set_err("out of pinned host memory"); return BSQ_E_NOMEM; }
+        s.host_cap = cap;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
+        memcpy(s.host + in_off[i], ns, 12 + 16 * (size_t)ns_holes_num(ns) + (size_t)(poff[i + 1] - poff[i]));
+    }
+    s.n = n_reads;
+    s.max_len = max_len;
+    s.bases = s.offs[n];
+    s.host_bytes = bytes;
+    return BSQ_OK;
+}
+
+int batch_upload_staged(bsq_batch *b, const NsStage &s)
+{
+    if (s.n > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
+    if (s.bases > b->max_bases) { set_err("batch holds at most %lld bases", (long long)b->max_bases); return BSQ_E_INVALID; }
+    HIPCHK(hipSetDevice(b->device));
+    const size_t n = (size_t)s.n;
+    { const int rc = grow_dev(b->ns_dev, b->ns_dev_cap, std::max<int64_t>(s.host_bytes, 1)); if (rc) return rc; }
+    { const int rc = grow_dev(b->ns_meta, b->ns_meta_cap, (int64_t)s.meta.size()); if (rc) return rc; }
+    b->h_offs = s.offs;
+    b->n_reads = s.n;
+    b->max_len = s.max_len;
+    if (n) {
+        hipStream_t st = b->stream;
+        HIPCHK(hipMemcpyAsync(b->ns_dev, s.host, (size_t)s.host_bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->ns_meta, s.meta.data(), s.meta.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->offs, s.offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const DecView v{b->ns_dev, b->ns_meta, b->ns_meta + n + 1, b->offs, (int64_t)n, s.meta[2 * n + 1]};
+        HIPCHK(launch_dec_codes(st, v, b->ns_meta + 2 * (n + 1), (int64_t)(s.meta.size() - 2 * (n + 1)), b->codes));
+    }
+    { const int rc = prepare_workspace(b, s.max_len); if (rc) return rc; }
+    HIPCHK(hipStreamSynchronize(b->stream));   // the staged buffers may be reused when this returns
+    return BSQ_OK;
+}
+
+}  // namespace bsq
+
 extern "C" int bsq_batch_set_nuclseqs(bsq_batch *b, const void *const *reads, int32_t n_reads)
 {
     if (!b || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
     if (n_reads > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
-    HIPCHK(hipSetDevice(b->device));
-    const size_t n = (size_t)n_reads;
-    std::vector<int64_t> meta(2 * (n + 1), 0);   // in_off | poff, then the holed reads
-    int64_t *in_off = meta.data(), *poff = meta.data() + n + 1;
-    b->h_offs.assign(n + 1, 0);
-    int max_len = 0;
-    for (size_t s = 0; s < n; ++s) {
-        const uint8_t *ns = static_cast<const uint8_t *>(reads[s]);
-        if (!ns) { set_err("read %zu is NULL", s); return BSQ_E_INVALID; }
-        uint32_t vl; memcpy(&vl, ns, 4);
-        const uint64_t nh = ns_holes_num(ns), len = ns_len(ns), need = 12 + 16 * nh + pac_byte_size(len);
-        if ((vl >> 2) < need) { set_err("read %zu: varlena of %u bytes, %llu needed", s, vl >> 2, (unsigned long long)need); return BSQ_E_INVALID; }
-        if (nh) meta.push_back((int64_t)s);
-        in_off = meta.data(); poff = meta.data() + n + 1;
-        in_off[s + 1] = in_off[s] + (int64_t)((need + 7) & ~7ull);
-        poff[s + 1] = poff[s] + (int64_t)pac_byte_size(len);
-        b->h_offs[s + 1] = b->h_offs[s] + (int64_t)len;
-        max_len = std::max<int>(max_len, (int)len);
-    }
-    const int64_t total = b->h_offs[n];
-    if (total > b->max_bases) { set_err("batch holds at most %lld bases", (long long)b->max_bases); return BSQ_E_INVALID; }
-    b->ns_host.resize((size_t)in_off[n]);
-    for (size_t s = 0; s < n; ++s) {
-        const uint8_t *ns = static_cast<const uint8_t *>(reads[s]);
-        memcpy(b->ns_host.data() + in_off[s], ns, 12 + 16 * (size_t)ns_holes_num(ns) + (size_t)(poff[s + 1] - poff[s]));
-    }
-    { const int rc = grow_dev(b->ns_dev, b->ns_dev_cap, (int64_t)b->ns_host.size()); if (rc) return rc; }
-    { const int rc = grow_dev(b->ns_meta, b->ns_meta_cap, (int64_t)meta.size()); if (rc) return rc; }
-    b->n_reads = n_reads;
-    b->max_len = max_len;
-    if (n_reads) {
-        hipStream_t st = b->stream;
-        HIPCHK(hipMemcpyAsync(b->ns_dev, b->ns_host.data(), b->ns_host.size(), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(b->ns_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(b->offs, b->h_offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-        const DecView v{b->ns_dev, b->ns_meta, b->ns_meta + n + 1, b->offs, (int64_t)n, poff[n]};
-        HIPCHK(launch_dec_codes(st, v, b->ns_meta + 2 * (n + 1), (int64_t)(meta.size() - 2 * (n + 1)), b->codes));
-    }
-    { const int rc = prepare_workspace(b, max_len); if (rc) return rc; }
-    HIPCHK(hipStreamSynchronize(b->stream));
-    return BSQ_OK;
+    { const int rc = stage_nuclseqs(b->stage, reads, n_reads); if (rc) return rc; }
+    return batch_upload_staged(b, b->stage);
 }
 
 // Runs smem -> chain -> extend -> reg2aln on workspace w for n local reads.
@@ -1762,11 +1801,8 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
 {
     if (!idx || !opts || !out || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
     *out = nullptr;
-    int64_t n_bases = 0;
-    for (int i = 0; i < n_reads; ++i) {
+    for (int i = 0; i < n_reads; ++i)
         if (!reads[i]) { set_err("read %d is NULL", i); return BSQ_E_INVALID; }
-        n_bases += ns_len(static_cast<const uint8_t *>(reads[i]));
-    }
     bsq_hits *h = (bsq_hits *)calloc(1, sizeof(bsq_hits));
     if (!h) { set_err("out of memory"); return BSQ_E_NOMEM; }
     h->n_reads = n_reads;
@@ -1777,41 +1813,94 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
         return BSQ_OK;
     }
     if (!idx->h.dev) { free(h); set_err("index not uploaded to a device (call bsq_index_upload)"); return BSQ_E_NODEV; }
-    // the index's pooled batch when it is free and large enough (its workspace is reused across calls)
-    bsq_batch *b = nullptr;
-    int rc = BSQ_OK;
+    // The call runs as up to `slots` concurrent sub-batches of the index's pipeline (pipeline.cpp): each slot's
+    // worker stages, uploads and aligns its share on its own stream, so the stages of one fill the tails of the
+    // others and the host staging runs in parallel.  The pipeline (and its workspaces) is kept across calls; a
+    // concurrent caller that finds it busy runs on a pipeline of its own.
+    const int slots = []() { const char *e = getenv("BSQ_PIPE_SLOTS"); const int v = e ? atoi(e) : 0; return v > 0 ? std::min(v, 16) : 4; }();
+    const int64_t min_chunk = 32768;   // smaller shares lose more to the stage tails than concurrency gains
+    const int k = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ((int64_t)n_reads + min_chunk - 1) / min_chunk));
     std::unique_lock<std::mutex> lk(idx->pool_mu, std::try_to_lock);
     const bool pooled = lk.owns_lock();
+    bsq_pipeline *p = nullptr;
+    int rc = BSQ_OK;
     if (pooled) {
-        if (idx->pool && (idx->pool->max_reads < n_reads || idx->pool->max_bases < n_bases)) {
-            bsq_batch_free(idx->pool);
-            idx->pool = nullptr;
+        if (!idx->pipe || bsq_pipeline_slots(idx->pipe) < k) {
+            bsq_pipeline_free(idx->pipe);
+            idx->pipe = nullptr;
+            rc = bsq_pipeline_create(idx, std::max(k, slots), &idx->pipe);
         }
-        if (!idx->pool) rc = bsq_batch_create(idx, n_reads, n_bases, &idx->pool);
-        b = idx->pool;
-    } else rc = bsq_batch_create(idx, n_reads, n_bases, &b);
-    if (rc == BSQ_OK) rc = bsq_batch_set_nuclseqs(b, reads, n_reads);
-    if (rc == BSQ_OK) rc = bsq_batch_run(b, opts, first_call_seq);
+        p = idx->pipe;
+    } else rc = bsq_pipeline_create(idx, k, &p);
+    std::vector<int32_t> lo((size_t)k + 1);
+    for (int j = 0; j <= k; ++j) lo[(size_t)j] = (int32_t)((int64_t)n_reads * j / k);
+    int submitted = 0;
+    for (int j = 0; j < k && rc == BSQ_OK; ++j) {
+        rc = pipeline_submit_ex(p, opts, reads + lo[(size_t)j], lo[(size_t)j + 1] - lo[(size_t)j],
+                                first_call_seq + (uint64_t)lo[(size_t)j], 0, PipeMode::DEFER);
+        if (rc == BSQ_OK) ++submitted;
+    }
+    std::vector<const bsq_hits *> v((size_t)k, nullptr);
+    std::string err;
+    for (int j = 0; j < submitted; ++j) {   // every submission is taken, failed or not
+        const int r = pipeline_next_ex(p, &v[(size_t)j], nullptr, nullptr, nullptr);
+        if (r && rc == BSQ_OK) { rc = r; err = g_err; }
+    }
+    auto release_all = [&] {
+        for (int j = 0; j < submitted; ++j) if (v[(size_t)j]) bsq_pipeline_release(p);
+        if (!pooled) bsq_pipeline_free(p);
+    };
     if (rc != BSQ_OK) {
-        if (pooled) { bsq_batch_free(idx->pool); idx->pool = nullptr; } else bsq_batch_free(b);
+        if (!err.empty()) g_err = err;
+        const std::string m = g_err;
+        release_all();
+        if (pooled) { bsq_pipeline_free(idx->pipe); idx->pipe = nullptr; }
+        g_err = m;
         free(h);
         return rc;
     }
-    h->n_hits = b->view.n_hits;
-    h->n_cigar = b->view.n_cigar;
+    std::vector<int64_t> hb((size_t)k + 1, 0), cb((size_t)k + 1, 0);
+    for (int j = 0; j < k; ++j) {
+        hb[(size_t)j + 1] = hb[(size_t)j] + v[(size_t)j]->n_hits;
+        cb[(size_t)j + 1] = cb[(size_t)j] + v[(size_t)j]->n_cigar;
+    }
+    if (cb[(size_t)k] > (int64_t)UINT32_MAX) {
+        release_all();
+        free(h);
+        set_err("call holds more than 2^32 CIGAR operations; split it into smaller batches");
+        return BSQ_E_UNSUPPORTED;
+    }
+    h->n_hits = hb[(size_t)k];
+    h->n_cigar = cb[(size_t)k];
     h->hits = (bsq_hit *)malloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
     h->cigar = (uint32_t *)malloc(4 * (size_t)std::max<int64_t>(h->n_cigar, 1));
     h->read_off = (int64_t *)malloc(8 * ((size_t)n_reads + 1));
     if (!h->hits || !h->cigar || !h->read_off) {
-        if (!pooled) bsq_batch_free(b);
+        release_all();
         bsq_hits_free(h);
         set_err("out of host memory for the hit records");
         return BSQ_E_NOMEM;
     }
-    memcpy(h->hits, b->view.hits, sizeof(bsq_hit) * (size_t)h->n_hits);
-    memcpy(h->cigar, b->view.cigar, 4 * (size_t)h->n_cigar);
-    memcpy(h->read_off, b->view.read_off, 8 * ((size_t)n_reads + 1));
-    if (!pooled) bsq_batch_free(b);
+    // merge in read order, one host thread per share: call-wide read indices and CIGAR offsets
+    auto copy_share = [&](int j) {
+        const bsq_hits &x = *v[(size_t)j];
+        bsq_hit *dst = h->hits + hb[(size_t)j];
+        if (x.n_hits) memcpy(dst, x.hits, sizeof(bsq_hit) * (size_t)x.n_hits);
+        for (int64_t i = 0; i < x.n_hits; ++i) {
+            dst[i].read_index += lo[(size_t)j];
+            dst[i].cigar_off += (uint32_t)cb[(size_t)j];
+        }
+        if (x.n_cigar) memcpy(h->cigar + cb[(size_t)j], x.cigar, 4 * (size_t)x.n_cigar);
+        for (int32_t r = 0; r < x.n_reads; ++r) h->read_off[lo[(size_t)j] + r] = hb[(size_t)j] + x.read_off[r] - x.read_off[0];
+    };
+    {
+        std::vector<std::thread> th;
+        for (int j = 1; j < k; ++j) th.emplace_back(copy_share, j);
+        copy_share(0);
+        for (auto &t : th) t.join();
+    }
+    h->read_off[n_reads] = h->n_hits;
+    release_all();
     *out = h;
     return BSQ_OK;
 }

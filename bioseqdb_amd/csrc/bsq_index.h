@@ -90,14 +90,15 @@ struct HostIndex {
 
 }  // namespace bsq
 
-// opaque C-ABI handle (include/bsq.h)
+// opaque C-ABI handles (include/bsq.h)
 struct bsq_batch;
-// the index plus one reusable batch for the one-shot bsq_align_batch (its workspace survives across calls;
-// a concurrent caller that finds it busy uses a batch of its own)
+struct bsq_pipeline;
+// the index plus one reusable pipeline of batches for the one-shot bsq_align_batch (its workspaces survive
+// across calls; a concurrent caller that finds it busy uses a pipeline of its own)
 struct bsq_index {
     bsq::HostIndex h;
     std::mutex pool_mu;
-    bsq_batch *pool = nullptr;
+    bsq_pipeline *pipe = nullptr;
     // offset-ordered holes for host rendering, built on first use after the index is built
     std::once_flag hx_once;
     std::unique_ptr<bsq::HoleIndex> hx;

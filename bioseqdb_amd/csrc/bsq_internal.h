@@ -1,0 +1,54 @@
+// bsq_internal.h -- library-internal C++ interface between bsq_api.cpp (batches) and the host drivers built on
+// top of them (pipeline.cpp, group.cpp).  Not part of the C-ABI (include/bsq.h).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/bsq.h"
+
+namespace bsq {
+
+// The host half of bsq_batch_set_nuclseqs: a cursor fetch's nuclseq varlenas validated and packed (8-byte
+// aligned, as they are) into pinned host memory, with the offsets the device decode pass needs.  Once staged,
+// the caller's varlenas may be released (the SPI tuple table of the fetch); the device half
+// (batch_upload_staged) runs later, on any thread.
+struct NsStage {
+    int32_t n = 0;
+    int max_len = 0;
+    int64_t bases = 0;
+    std::vector<int64_t> meta;    // in_off[n+1] | poff[n+1] | indices of the reads with holes
+    std::vector<int64_t> offs;    // base offsets [n+1]
+    uint8_t *host = nullptr;      // packed varlenas (pinned)
+    int64_t host_cap = 0, host_bytes = 0;
+    NsStage() = default;
+    NsStage(const NsStage &) = delete;
+    NsStage &operator=(const NsStage &) = delete;
+    ~NsStage();
+};
+
+// Validates and packs n reads (errors: BSQ_E_INVALID / BSQ_E_NOMEM with the thread's message set).
+int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n);
+// H2D of a staged fetch into batch b, nt4 conversion on the device, workspace sizing; synchronous.
+int batch_upload_staged(bsq_batch *b, const NsStage &s);
+int32_t batch_max_reads(const bsq_batch *b);
+int64_t batch_max_bases(const bsq_batch *b);
+
+void set_error(const std::string &msg);
+
+// pipeline.cpp: how a submission's reads reach the slot.  COPY: staged on the caller's thread before submit
+// returns (the public bsq_pipeline_submit).  DEFER: staged by the slot's worker (the reads must stay valid
+// until the submission is taken; lets a caller that holds all reads stage several slots in parallel).  RERUN:
+// the slot's previous staging again (the reads stay on the device: a benchmark's re-run of the same fetch).
+enum class PipeMode { COPY, DEFER, RERUN };
+int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                       uint64_t first_call_seq, int nuclseq_columns, PipeMode mode);
+// With nothing outstanding, the next submission goes to slot 0 again (a caller that submits shares j = 0..s-1 per
+// round keeps share j on slot j, where a RERUN finds its staging).  BSQ_E_INVALID while submissions are pending.
+int pipeline_rewind(bsq_pipeline *p);
+// bsq_pipeline_next plus the batch that holds the taken submission's records (NULL for an empty one)
+int pipeline_next_ex(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off,
+                     bsq_batch **batch);
+
+}  // namespace bsq

@@ -13,7 +13,13 @@
 // (bioseqdb_amd/dist.py, bench.py --gpus N) is different -- there the other ranks cannot hand host memory to
 // the caller, so its exchange step is an RCCL gather.
 //
-// Built only on the public C-ABI of bsq_api.cpp plus RCCL.
+// Every member aligns its shard as up to `slots` concurrent shares on a pipeline of its own (pipeline.cpp), so a
+// member keeps its device as busy as the one-GPU bench's concurrent batches do.  The records stay where the
+// members' pipelines put them -- pinned host memory, one segment per share, in read order -- until the caller
+// asks for the merged view (bsq_group_hits merges on first use, one host thread per segment) or walks the
+// segments itself (bsq_group_segments, zero-copy).
+//
+// Built on the public C-ABI of bsq_api.cpp plus RCCL and the pipeline internals (bsq_internal.h).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -27,8 +33,14 @@
 #include <vector>
 
 #include "../../include/bsq.h"
+#include "bsq_internal.h"
 
 extern "C" void bsq_internal_set_error(const char *msg);   // bsq_api.cpp: the message bsq_last_error() returns
+
+using bsq::PipeMode;
+using bsq::pipeline_next_ex;
+using bsq::pipeline_submit_ex;
+using bsq::pipeline_rewind;
 
 namespace {
 
@@ -46,10 +58,11 @@ struct Member {
     hipStream_t stream = nullptr;
     bsq_index *index = nullptr;          // member 0: the caller's index; others: imported replica
     std::vector<void *> bufs;            // replica tables (owned, members >= 1)
-    bsq_batch *batch = nullptr;
-    int32_t cap_reads = 0;
-    int64_t cap_bases = 0;
+    bsq_pipeline *pipe = nullptr;        // this member's concurrent shares (created at replicate)
     int32_t lo = 0, n = 0;               // shard of the last run
+    std::vector<int32_t> slo;            // shares of the shard: [slo[j], slo[j+1]) relative to lo
+    std::vector<const bsq_hits *> views; // taken (held) results of the shares, until the next run
+    std::vector<bsq_batch *> batches;    // the batch holding each share's records (NULL: no rows)
 };
 
 }  // namespace
@@ -58,7 +71,9 @@ struct bsq_group {
     std::vector<Member> m;
     bool rccl = false;                   // distinct devices: RCCL communicators; a repeated device: D2D copies
     bsq_index *src = nullptr;
+    int slots = 4;                       // concurrent shares per member (bsq_group_set_slots)
     int32_t n_reads = 0;
+    bool merged = false;                 // hits/cigar/read_off hold the last run's segments
     std::vector<bsq_hit> hits;
     std::vector<uint32_t> cigar;
     std::vector<int64_t> read_off;
@@ -67,14 +82,24 @@ struct bsq_group {
 
 namespace {
 
+void release_held(Member &x)
+{
+    for (size_t j = 0; j < x.views.size(); ++j) bsq_pipeline_release(x.pipe);
+    x.views.clear();
+    x.batches.clear();
+}
+
 void drop_replicas(bsq_group *g)
 {
+    g->merged = false;
+    g->view = bsq_hits{};
     for (size_t k = 0; k < g->m.size(); ++k) {
         Member &x = g->m[k];
-        bsq_batch_free(x.batch);
-        x.batch = nullptr;
-        x.cap_reads = 0;
-        x.cap_bases = 0;
+        release_held(x);
+        bsq_pipeline_free(x.pipe);
+        x.pipe = nullptr;
+        x.n = 0;
+        x.slo.clear();
         if (k > 0) {
             bsq_index_free(x.index);
             hipSetDevice(x.device);
@@ -231,6 +256,18 @@ extern "C" int bsq_group_replicate(bsq_group *g, bsq_index *idx, double *broadca
         const int rc = bsq_index_import(meta.data(), meta_bytes, x.device, tab, BSQ_N_TABLES, &x.index);
         if (rc) { const std::string m = bsq_last_error(); drop_replicas(g); return fail(rc, m); }
     }
+    for (size_t k = 0; k < G; ++k) {
+        const int rc = bsq_pipeline_create(g->m[k].index, g->slots, &g->m[k].pipe);
+        if (rc) { const std::string m = bsq_last_error(); drop_replicas(g); return fail(rc, m); }
+    }
+    return BSQ_OK;
+}
+
+extern "C" int bsq_group_set_slots(bsq_group *g, int slots)
+{
+    if (!g || slots < 1 || slots > 16) return fail(BSQ_E_INVALID, "invalid argument");
+    if (g->src) return fail(BSQ_E_INVALID, "set the slots before bsq_group_replicate");
+    g->slots = slots;
     return BSQ_OK;
 }
 
@@ -240,83 +277,126 @@ extern "C" int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *con
     if (!g || !opts) return fail(BSQ_E_INVALID, "invalid argument");
     if (!g->src) return fail(BSQ_E_INVALID, "no index replicated on the group (bsq_group_replicate)");
     const size_t G = g->m.size();
+    g->merged = false;
+    g->view = bsq_hits{};
+    for (Member &x : g->m) release_held(x);
     if (reads) {
         if (n_reads < 0) return fail(BSQ_E_INVALID, "invalid argument");
         for (int32_t i = 0; i < n_reads; ++i)
             if (!reads[i]) return fail(BSQ_E_INVALID, "read " + std::to_string(i) + " is NULL");
         g->n_reads = n_reads;
+        const int64_t min_share = 32768;   // smaller shares lose more to stage tails than concurrency gains
         for (size_t k = 0; k < G; ++k) {
-            g->m[k].lo = (int32_t)((int64_t)n_reads * (int64_t)k / (int64_t)G);
-            g->m[k].n = (int32_t)((int64_t)n_reads * (int64_t)(k + 1) / (int64_t)G) - g->m[k].lo;
+            Member &x = g->m[k];
+            x.lo = (int32_t)((int64_t)n_reads * (int64_t)k / (int64_t)G);
+            x.n = (int32_t)((int64_t)n_reads * (int64_t)(k + 1) / (int64_t)G) - x.lo;
+            const int s = (int)std::max<int64_t>(1, std::min<int64_t>(g->slots, ((int64_t)x.n + min_share - 1) / min_share));
+            x.slo.assign((size_t)s + 1, 0);
+            for (int j = 0; j <= s; ++j) x.slo[(size_t)j] = (int32_t)((int64_t)x.n * j / s);
         }
     } else if (n_reads != g->n_reads) return fail(BSQ_E_INVALID, "re-run of a different read count");
     const int rc = for_members(g, [&](int k) -> int {
         Member &x = g->m[(size_t)k];
         if (x.n == 0) return BSQ_OK;
-        if (reads) {
-            int64_t bases = 0;
-            for (int32_t i = 0; i < x.n; ++i) {
-                uint32_t len;
-                memcpy(&len, static_cast<const uint8_t *>(reads[x.lo + i]) + 8, 4);   // sequence.h:18-38 len
-                bases += len;
-            }
-            if (!x.batch || x.cap_reads < x.n || x.cap_bases < bases) {
-                bsq_batch_free(x.batch);
-                x.batch = nullptr;
-                x.cap_reads = std::max(x.n, 2 * x.cap_reads);
-                x.cap_bases = std::max(bases, 2 * x.cap_bases);
-                const int r = bsq_batch_create(x.index, x.cap_reads, x.cap_bases, &x.batch);
-                if (r) { x.cap_reads = 0; x.cap_bases = 0; return r; }
-            }
-            const int r = bsq_batch_set_nuclseqs(x.batch, reads + x.lo, x.n);
-            if (r) return r;
+        const int s = (int)x.slo.size() - 1;
+        int rc = pipeline_rewind(x.pipe), submitted = 0;   // share j on slot j (a re-run finds its staging there)
+        for (int j = 0; j < s && rc == BSQ_OK; ++j) {
+            const int32_t a = x.lo + x.slo[(size_t)j], n = x.slo[(size_t)j + 1] - x.slo[(size_t)j];
+            rc = reads ? pipeline_submit_ex(x.pipe, opts, reads + a, n, first_call_seq + (uint64_t)a, 0, PipeMode::DEFER)
+                       : pipeline_submit_ex(x.pipe, opts, nullptr, n, first_call_seq + (uint64_t)a, 0, PipeMode::RERUN);
+            if (rc == BSQ_OK) ++submitted;
         }
-        return bsq_batch_run(x.batch, opts, first_call_seq + (uint64_t)x.lo);
+        std::string err;
+        for (int j = 0; j < submitted; ++j) {   // every submission is taken, failed or not
+            const bsq_hits *v = nullptr;
+            bsq_batch *b = nullptr;
+            const int r = pipeline_next_ex(x.pipe, &v, nullptr, nullptr, &b);
+            if (r) { if (rc == BSQ_OK) { rc = r; err = bsq_last_error(); } continue; }
+            x.views.push_back(v);
+            x.batches.push_back(b);
+        }
+        if (rc != BSQ_OK) {
+            if (!err.empty()) bsq_internal_set_error(err.c_str());
+            const std::string m = bsq_last_error();
+            release_held(x);
+            bsq_internal_set_error(m.c_str());
+        }
+        return rc;
     });
-    if (rc) return rc;
-    // merge in member (= read) order: batch-wide read indices and CIGAR offsets
-    int64_t nh = 0, nc = 0;
-    std::vector<int64_t> hb(G + 1, 0), cb(G + 1, 0);
-    for (size_t k = 0; k < G; ++k) {
-        const bsq_hits *v = g->m[k].n ? bsq_batch_hits(g->m[k].batch) : nullptr;
-        hb[k + 1] = hb[k] + (v ? v->n_hits : 0);
-        cb[k + 1] = cb[k] + (v ? v->n_cigar : 0);
+    if (rc) {
+        for (Member &x : g->m) release_held(x);
+        return rc;
     }
-    nh = hb[G];
-    nc = cb[G];
-    try {
-        g->hits.resize((size_t)nh);
-        g->cigar.resize((size_t)nc);
-        g->read_off.resize((size_t)g->n_reads + 1);
-    } catch (const std::bad_alloc &) {
-        return fail(BSQ_E_NOMEM, "out of host memory for the merged records");
+    int64_t nc = 0;
+    for (const Member &x : g->m)
+        for (const bsq_hits *v : x.views) nc += v->n_cigar;
+    if ((uint64_t)nc > UINT32_MAX) {
+        for (Member &x : g->m) release_held(x);
+        return fail(BSQ_E_UNSUPPORTED, "more than 2^32 CIGAR operations in one call");
     }
-    g->read_off[0] = 0;
-    for (size_t k = 0; k < G; ++k) {
-        const Member &x = g->m[k];
-        if (!x.n) continue;
-        const bsq_hits *v = bsq_batch_hits(x.batch);
-        if ((uint64_t)cb[k] + (uint64_t)v->n_cigar > UINT32_MAX)
-            return fail(BSQ_E_UNSUPPORTED, "more than 2^32 CIGAR operations in one call");
-        bsq_hit *dst = g->hits.data() + hb[k];
-        if (v->n_hits) memcpy(dst, v->hits, sizeof(bsq_hit) * (size_t)v->n_hits);
-        for (int64_t i = 0; i < v->n_hits; ++i) {
-            dst[i].read_index += x.lo;
-            dst[i].cigar_off += (uint32_t)cb[k];
-        }
-        if (v->n_cigar) memcpy(g->cigar.data() + cb[k], v->cigar, 4 * (size_t)v->n_cigar);
-        for (int32_t i = 1; i <= x.n; ++i) g->read_off[(size_t)x.lo + (size_t)i] = hb[k] + v->read_off[i] - v->read_off[0];
-    }
-    g->view.n_reads = g->n_reads;
-    g->view.n_hits = nh;
-    g->view.hits = g->hits.data();
-    g->view.read_off = g->read_off.data();
-    g->view.n_cigar = nc;
-    g->view.cigar = g->cigar.data();
     return BSQ_OK;
 }
 
-extern "C" const bsq_hits *bsq_group_hits(const bsq_group *g) { return g ? &g->view : nullptr; }
+extern "C" int bsq_group_segments(const bsq_group *g, const bsq_hits **views, int32_t *read_lo, int max)
+{
+    if (!g || max < 0 || (max > 0 && (!views || !read_lo))) return fail(BSQ_E_INVALID, "invalid argument");
+    int n = 0;
+    for (const Member &x : g->m)
+        for (size_t j = 0; j < x.views.size(); ++j, ++n)
+            if (n < max) { views[n] = x.views[j]; read_lo[n] = x.lo + x.slo[j]; }
+    return n;
+}
+
+// the merged view of the last run (segments concatenated in read order; one host thread per segment)
+static int merge(bsq_group *g)
+{
+    std::vector<const bsq_hits *> v;
+    std::vector<int32_t> rlo;
+    for (const Member &x : g->m)
+        for (size_t j = 0; j < x.views.size(); ++j) { v.push_back(x.views[j]); rlo.push_back(x.lo + x.slo[j]); }
+    const size_t S = v.size();
+    std::vector<int64_t> hb(S + 1, 0), cb(S + 1, 0);
+    for (size_t j = 0; j < S; ++j) { hb[j + 1] = hb[j] + v[j]->n_hits; cb[j + 1] = cb[j] + v[j]->n_cigar; }
+    try {
+        g->hits.resize((size_t)hb[S]);
+        g->cigar.resize((size_t)cb[S]);
+        g->read_off.assign((size_t)g->n_reads + 1, 0);
+    } catch (const std::bad_alloc &) {
+        return fail(BSQ_E_NOMEM, "out of host memory for the merged records");
+    }
+    auto one = [&](size_t j) {
+        const bsq_hits &x = *v[j];
+        bsq_hit *dst = g->hits.data() + hb[j];
+        if (x.n_hits) memcpy(dst, x.hits, sizeof(bsq_hit) * (size_t)x.n_hits);
+        for (int64_t i = 0; i < x.n_hits; ++i) {
+            dst[i].read_index += rlo[j];
+            dst[i].cigar_off += (uint32_t)cb[j];
+        }
+        if (x.n_cigar) memcpy(g->cigar.data() + cb[j], x.cigar, 4 * (size_t)x.n_cigar);
+        for (int32_t i = 0; i < x.n_reads; ++i) g->read_off[(size_t)rlo[j] + (size_t)i] = hb[j] + x.read_off[i] - x.read_off[0];
+    };
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < S; ++j) th.emplace_back(one, j);
+    if (S) one(0);
+    for (auto &t : th) t.join();
+    g->read_off[(size_t)g->n_reads] = hb[S];
+    g->view.n_reads = g->n_reads;
+    g->view.n_hits = hb[S];
+    g->view.hits = g->hits.data();
+    g->view.read_off = g->read_off.data();
+    g->view.n_cigar = cb[S];
+    g->view.cigar = g->cigar.data();
+    g->merged = true;
+    return BSQ_OK;
+}
+
+extern "C" const bsq_hits *bsq_group_hits(const bsq_group *cg)
+{
+    if (!cg) return nullptr;
+    bsq_group *g = const_cast<bsq_group *>(cg);   // the merge is a cache of the segments
+    if (!g->merged && g->src && merge(g) != BSQ_OK) return nullptr;
+    return &g->view;
+}
 
 extern "C" int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads, uint8_t **out, int64_t **out_off)
 {
@@ -324,34 +404,38 @@ extern "C" int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads,
     *out = nullptr;
     *out_off = nullptr;
     const size_t G = g->m.size();
-    std::vector<uint8_t *> part(G, nullptr);
-    std::vector<int64_t *> poff(G, nullptr);
+    struct Part { uint8_t *buf = nullptr; int64_t *off = nullptr; int64_t nv = 0; };
+    std::vector<std::vector<Part>> part(G);
+    for (size_t k = 0; k < G; ++k) part[k].resize(g->m[k].views.size());
     const int rc = for_members(g, [&](int k) -> int {
         const Member &x = g->m[(size_t)k];
-        if (!x.n) return BSQ_OK;
-        return bsq_batch_render_nuclseqs(x.batch, reads + x.lo, &part[(size_t)k], &poff[(size_t)k]);
+        for (size_t j = 0; j < x.views.size(); ++j) {
+            if (!x.batches[j] || !x.views[j]->n_hits) continue;
+            Part &q = part[(size_t)k][j];
+            q.nv = 2 * x.views[j]->n_hits;
+            const int r = bsq_batch_render_nuclseqs(x.batches[j], reads + x.lo + x.slo[j], &q.buf, &q.off);
+            if (r) return r;
+        }
+        return BSQ_OK;
     });
-    auto release = [&] { for (size_t k = 0; k < G; ++k) { bsq_free(part[k]); bsq_free(poff[k]); } };
+    auto release = [&] { for (auto &v : part) for (Part &q : v) { bsq_free(q.buf); bsq_free(q.off); } };
     if (rc) { release(); return rc; }
-    const int64_t nv = 2 * g->view.n_hits;
-    std::vector<int64_t> base(G + 1, 0);   // byte offset of member k's varlenas (8-byte aligned)
-    for (size_t k = 0; k < G; ++k) {
-        const int64_t nk = g->m[k].n ? 2 * bsq_batch_hits(g->m[k].batch)->n_hits : 0;
-        const int64_t bytes = nk ? poff[k][nk] : 0;
-        base[k + 1] = base[k] + ((bytes + 7) & ~7LL);
-    }
-    uint8_t *buf = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(base[G], 1)));
+    int64_t nv = 0, bytes = 0;
+    for (auto &v : part)
+        for (Part &q : v) { nv += q.nv; bytes += q.nv ? ((q.off[q.nv] + 7) & ~7LL) : 0; }
+    uint8_t *buf = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(bytes, 1)));
     int64_t *off = static_cast<int64_t *>(malloc(((size_t)nv + 1) * 8));
     if (!buf || !off) { free(buf); free(off); release(); return fail(BSQ_E_NOMEM, "out of host memory"); }
-    int64_t v0 = 0;
-    for (size_t k = 0; k < G; ++k) {
-        const int64_t nk = g->m[k].n ? 2 * bsq_batch_hits(g->m[k].batch)->n_hits : 0;
-        if (!nk) continue;
-        memcpy(buf + base[k], part[k], (size_t)poff[k][nk]);
-        for (int64_t i = 0; i < nk; ++i) off[v0 + i] = base[k] + poff[k][i];
-        v0 += nk;
-    }
-    off[nv] = base[G];
+    int64_t v0 = 0, base = 0;
+    for (auto &v : part)
+        for (Part &q : v) {
+            if (!q.nv) continue;
+            memcpy(buf + base, q.buf, (size_t)q.off[q.nv]);
+            for (int64_t i = 0; i < q.nv; ++i) off[v0 + i] = base + q.off[i];
+            v0 += q.nv;
+            base += (q.off[q.nv] + 7) & ~7LL;
+        }
+    off[nv] = base;
     release();
     *out = buf;
     *out_off = off;

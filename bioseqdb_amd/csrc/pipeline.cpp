@@ -1,0 +1,287 @@
+// pipeline.cpp -- cursor fetches aligned as a pipeline of batches (include/bsq.h bsq_pipeline_*).
+//
+// The reference aligns a query cursor one row at a time, each row through the whole of libbwa before the next
+// fetch (bioseqdb/extension.cpp:156-195, 362-370).  On the GPU a fetch is one batch, and a lone batch leaves the
+// device idle while the backend fetches the next rows, stages them and builds the previous fetch's tuples, and
+// leaves the CUs under-filled in the stage tails of its own kernels.  A pipeline owns n_slots batches, each
+// with its own HIP stream and host worker thread: submit() stages a fetch (its tuples may be released as soon
+// as it returns) and hands it to the next slot's worker, which uploads, aligns, copies the records to pinned
+// host memory and, if asked, renders the two nuclseq columns of every row on the GPU.  Results come back in
+// submission order (next/release), so up to n_slots fetches are on the device at once while the caller
+// produces the next fetch and consumes the last one.  The one-shot bsq_align_batch splits a large call over
+// its index's pipeline the same way, and every member of a device group owns one (group.cpp).
+//
+// Built on the C-ABI of bsq_api.cpp plus its staging halves (bsq_internal.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/bsq.h"
+#include "bsq_internal.h"
+
+using namespace bsq;
+
+namespace {
+
+enum class SlotState { FREE, QUEUED, DONE, HELD };
+
+struct Slot {
+    SlotState state = SlotState::FREE;
+    // job
+    bsq_opts opts{};
+    uint64_t first_call = 0;
+    int32_t n = 0;
+    bool cols = false;
+    PipeMode mode = PipeMode::COPY;
+    const void *const *reads = nullptr;   // PipeMode::DEFER: staged by the worker
+    // batch and staging
+    bsq_batch *batch = nullptr;
+    int32_t cap_reads = 0;
+    int64_t cap_bases = 0;
+    NsStage stage;
+    bool resident = false;                // the batch holds this staging's reads (a RERUN skips the upload)
+    // result
+    int rc = BSQ_OK;
+    std::string err;
+    const bsq_hits *view = nullptr;
+    bsq_hits empty{};
+    std::vector<int64_t> zeros;
+    uint8_t *col_buf = nullptr;
+    int64_t *col_off = nullptr;
+    std::thread th;
+};
+
+}  // namespace
+
+struct bsq_pipeline {
+    bsq_index *idx = nullptr;
+    std::vector<std::unique_ptr<Slot>> s;
+    uint64_t n_submit = 0, n_take = 0, n_release = 0;   // slot of job j is s[j % S]
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stop = false;
+};
+
+namespace {
+
+void drop_cols(Slot &x)
+{
+    bsq_free(x.col_buf);
+    bsq_free(x.col_off);
+    x.col_buf = nullptr;
+    x.col_off = nullptr;
+}
+
+// The job of one slot, on its worker thread.
+int run_job(bsq_pipeline *p, Slot &x)
+{
+    if (x.mode == PipeMode::DEFER) {
+        x.resident = false;
+        const int rc = stage_nuclseqs(x.stage, x.reads, x.n);
+        if (rc) return rc;
+    } else if (x.mode == PipeMode::COPY) {
+        x.resident = false;
+    }
+    if (x.n == 0 || bsq_index_seq_len(p->idx) <= 0) {   // bwa.cpp:142-143: no region for any read
+        x.zeros.assign((size_t)x.n + 1, 0);
+        x.empty = bsq_hits{};
+        x.empty.n_reads = x.n;
+        x.empty.read_off = x.zeros.data();
+        x.view = &x.empty;
+        return BSQ_OK;
+    }
+    if (!x.batch || x.cap_reads < x.stage.n || x.cap_bases < x.stage.bases) {
+        bsq_batch_free(x.batch);
+        x.batch = nullptr;
+        x.resident = false;
+        // grow geometrically so fetches of similar size reuse one workspace
+        const int32_t r = std::max<int32_t>(x.stage.n, (int32_t)std::min<int64_t>(2LL * x.cap_reads, 1 << 20));
+        const int64_t b = std::max<int64_t>(x.stage.bases, std::min<int64_t>(2 * x.cap_bases, (int64_t)r * 1024));
+        const int rc = bsq_batch_create(p->idx, std::max(r, 1), std::max<int64_t>(b, 1), &x.batch);
+        if (rc) { x.batch = nullptr; x.cap_reads = 0; x.cap_bases = 0; return rc; }
+        x.cap_reads = std::max(r, 1);
+        x.cap_bases = std::max<int64_t>(b, 1);
+    }
+    if (!x.resident) {
+        const int rc = batch_upload_staged(x.batch, x.stage);
+        if (rc) return rc;
+        x.resident = true;
+    }
+    { const int rc = bsq_batch_run(x.batch, &x.opts, x.first_call); if (rc) return rc; }
+    x.view = bsq_batch_hits(x.batch);
+    if (x.cols && x.view->n_hits > 0) {
+        // the staged varlenas carry the reads' hole symbols (the caller's may be gone)
+        std::vector<const void *> ptrs((size_t)x.n);
+        for (int32_t i = 0; i < x.n; ++i) ptrs[(size_t)i] = x.stage.host + x.stage.meta[(size_t)i];
+        const int rc = bsq_batch_render_nuclseqs(x.batch, ptrs.data(), &x.col_buf, &x.col_off);
+        if (rc) return rc;
+    }
+    return BSQ_OK;
+}
+
+void worker(bsq_pipeline *p, Slot *x)
+{
+    std::unique_lock<std::mutex> lk(p->mu);
+    for (;;) {
+        p->cv.wait(lk, [&] { return p->stop || x->state == SlotState::QUEUED; });
+        if (p->stop) return;
+        lk.unlock();
+        const int rc = run_job(p, *x);
+        const std::string err = rc ? std::string(bsq_last_error()) : std::string();
+        lk.lock();
+        x->rc = rc;
+        x->err = err;
+        x->state = SlotState::DONE;
+        p->cv.notify_all();
+    }
+}
+
+int fail(int rc, const std::string &m)
+{
+    set_error(m);
+    return rc;
+}
+
+}  // namespace
+
+namespace bsq {
+
+int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                       uint64_t first_call_seq, int nuclseq_columns, PipeMode mode)
+{
+    if (!p || !opts || n_reads < 0 || (n_reads && !reads && mode != PipeMode::RERUN)) return fail(BSQ_E_INVALID, "invalid argument");
+    if (opts->e_del <= 0 || opts->e_ins <= 0 || opts->max_occ <= 0 || opts->min_seed_len < 0)
+        return fail(BSQ_E_INVALID, "gap extension penalties and max_occ must be positive, min_seed_len nonnegative");
+    Slot *x;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        x = p->s[p->n_submit % p->s.size()].get();
+        if (x->state != SlotState::FREE)
+            return fail(BSQ_E_INVALID, "every slot of the pipeline holds a submission (take and release the oldest first)");
+    }
+    if (mode == PipeMode::RERUN && x->stage.n != n_reads)
+        return fail(BSQ_E_INVALID, "re-run of a different read count than the slot's staged reads");
+    if (mode == PipeMode::COPY) {   // staged on the caller's thread: the caller may release its reads on return
+        x->resident = false;
+        const int rc = stage_nuclseqs(x->stage, reads, n_reads);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    x->opts = *opts;
+    x->first_call = first_call_seq;
+    x->n = n_reads;
+    x->cols = nuclseq_columns != 0;
+    x->mode = mode;
+    x->reads = mode == PipeMode::DEFER ? reads : nullptr;
+    x->view = nullptr;
+    drop_cols(*x);
+    x->state = SlotState::QUEUED;
+    ++p->n_submit;
+    p->cv.notify_all();
+    return BSQ_OK;
+}
+
+int pipeline_rewind(bsq_pipeline *p)
+{
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->n_release != p->n_submit) return fail(BSQ_E_INVALID, "pipeline has outstanding submissions");
+    p->n_submit = p->n_take = p->n_release = 0;
+    return BSQ_OK;
+}
+
+int pipeline_next_ex(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off,
+                     bsq_batch **batch)
+{
+    if (!p || !view) return fail(BSQ_E_INVALID, "invalid argument");
+    std::unique_lock<std::mutex> lk(p->mu);
+    if (p->n_take == p->n_submit) return fail(BSQ_E_INVALID, "no submission to take");
+    Slot *x = p->s[p->n_take % p->s.size()].get();
+    p->cv.wait(lk, [&] { return x->state == SlotState::DONE; });
+    ++p->n_take;
+    if (x->rc) {   // consumed: the slot is free again (its submission produced no rows)
+        const int rc = x->rc;
+        const std::string m = x->err;
+        x->state = SlotState::HELD;
+        lk.unlock();
+        bsq_pipeline_release(p);
+        return fail(rc, m);
+    }
+    x->state = SlotState::HELD;
+    *view = x->view;
+    if (cols) *cols = x->col_buf;
+    if (col_off) *col_off = x->col_off;
+    if (batch) *batch = x->view == &x->empty ? nullptr : x->batch;
+    return BSQ_OK;
+}
+
+}  // namespace bsq
+
+extern "C" int bsq_pipeline_create(bsq_index *idx, int n_slots, bsq_pipeline **out)
+{
+    if (!idx || !out || n_slots < 1 || n_slots > 64) return fail(BSQ_E_INVALID, "invalid argument");
+    *out = nullptr;
+    std::unique_ptr<bsq_pipeline> p(new (std::nothrow) bsq_pipeline());
+    if (!p) return fail(BSQ_E_NOMEM, "out of memory");
+    p->idx = idx;
+    for (int k = 0; k < n_slots; ++k) p->s.emplace_back(new Slot());
+    for (auto &x : p->s) x->th = std::thread(worker, p.get(), x.get());
+    *out = p.release();
+    return BSQ_OK;
+}
+
+extern "C" void bsq_pipeline_free(bsq_pipeline *p)
+{
+    if (!p) return;
+    {
+        std::unique_lock<std::mutex> lk(p->mu);
+        // submissions still on the device finish first (their workers own the batches)
+        p->cv.wait(lk, [&] {
+            for (auto &x : p->s)
+                if (x->state == SlotState::QUEUED) return false;
+            return true;
+        });
+        p->stop = true;
+        p->cv.notify_all();
+    }
+    for (auto &x : p->s) {
+        if (x->th.joinable()) x->th.join();
+        drop_cols(*x);
+        bsq_batch_free(x->batch);
+    }
+    delete p;
+}
+
+extern "C" int bsq_pipeline_slots(const bsq_pipeline *p) { return p ? (int)p->s.size() : 0; }
+
+extern "C" int bsq_pipeline_submit(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                                   uint64_t first_call_seq, int nuclseq_columns)
+{
+    return pipeline_submit_ex(p, opts, reads, n_reads, first_call_seq, nuclseq_columns, PipeMode::COPY);
+}
+
+extern "C" int bsq_pipeline_next(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off)
+{
+    return pipeline_next_ex(p, view, cols, col_off, nullptr);
+}
+
+extern "C" int bsq_pipeline_release(bsq_pipeline *p)
+{
+    if (!p) return fail(BSQ_E_INVALID, "invalid argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->n_release == p->n_take) return fail(BSQ_E_INVALID, "no taken submission to release");
+    Slot *x = p->s[p->n_release % p->s.size()].get();
+    drop_cols(*x);
+    x->view = nullptr;
+    x->state = SlotState::FREE;
+    ++p->n_release;
+    p->cv.notify_all();
+    return BSQ_OK;
+}

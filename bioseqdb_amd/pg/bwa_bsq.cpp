@@ -62,19 +62,20 @@ BwaIndex::BwaIndex(const std::vector<int> &devices)
 }
 
 BwaIndex::BwaIndex(BwaIndex &&o) noexcept
-    : options(o.options), index_(o.index_), devices_(o.devices_), group_(o.group_), batch_(o.batch_),
-      batch_reads_(o.batch_reads_), batch_bases_(o.batch_bases_), rows_(std::move(o.rows_))
+    : options(o.options), index_(o.index_), devices_(o.devices_), group_(o.group_), pipe_(o.pipe_)
 {
+    o.reset_rows();   // a moved-from index keeps no submissions; the pipeline moves empty
     o.options = nullptr;
     o.index_ = nullptr;
     o.group_ = nullptr;
-    o.batch_ = nullptr;
+    o.pipe_ = nullptr;
 }
 
 BwaIndex::~BwaIndex()
 {
     rows_ = BwaRows();
-    bsq_batch_free(batch_);
+    group_rows_ = BwaRows();
+    bsq_pipeline_free(pipe_);   // waits for submissions still on the device
     bsq_group_free(group_);
     bsq_index_free(index_);
     delete options;
@@ -93,19 +94,19 @@ void BwaIndex::build()
     else check(bsq_index_build(index_, 0));   // same tables; aligning then reports the missing device
 }
 
-void BwaIndex::ensure_batch(int32_t n, int64_t bases) const
+int BwaIndex::pipeline_depth() const
 {
-    if (batch_ && batch_reads_ >= n && batch_bases_ >= bases) return;
+    if (devices_.size() > 1) return 1;   // a group aligns its fetch at submit (every member pipelines its shard)
+    const char *e = getenv("BSQ_PIPE_DEPTH");
+    const int d = e ? atoi(e) : 3;
+    return std::max(1, std::min(d, 16));
+}
+
+void BwaIndex::ensure_pipe() const
+{
+    if (pipe_) return;
     check(bsq_index_upload(index_, device()));   // no-op for an index built on the device
-    rows_ = BwaRows();
-    bsq_batch_free(batch_);
-    batch_ = nullptr;
-    // grow geometrically so a cursor's fetches of similar size reuse one workspace
-    const int32_t r = std::max<int32_t>(n, std::min<int64_t>(2LL * batch_reads_, 1 << 20));
-    const int64_t b = std::max<int64_t>(bases, std::min<int64_t>(2 * batch_bases_, (int64_t)r * 1024));
-    check(bsq_batch_create(index_, std::max(r, 1), std::max<int64_t>(b, 1), &batch_));
-    batch_reads_ = std::max(r, 1);
-    batch_bases_ = std::max<int64_t>(b, 1);
+    check(bsq_pipeline_create(index_, pipeline_depth(), &pipe_));
 }
 
 void BwaIndex::ensure_group() const
@@ -123,46 +124,118 @@ void BwaIndex::ensure_group() const
     group_ = g;
 }
 
-const BwaRows &BwaIndex::align_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
-                                    const BsqMemOpt *opts) const
+void BwaIndex::submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
+                           const BsqMemOpt *opts) const
 {
-    std::lock_guard<std::mutex> lk(mu_);
-    rows_ = BwaRows();
+    if ((int)pending_.size() + held_ >= pipeline_depth())
+        throw BsqFailure(BSQ_E_INVALID, "every pipeline slot holds a fetch (take and release the oldest first)");
+    Pending pd;
+    pd.cols = nuclseq_columns;
+    pd.n = std::max(n, 0);
     if (n <= 0 || empty()) {   // bwa.cpp:142-143: no mem_align1 call, no lrand48 value drawn
-        static thread_local std::vector<int64_t> zeros;
-        static thread_local bsq_hits none;
-        zeros.assign((size_t)std::max(n, 0) + 1, 0);
-        none = kNoHits;
-        none.n_reads = std::max(n, 0);
-        none.read_off = zeros.data();
-        rows_.view_ = &none;
-        return rows_;
+        pd.empty = true;
+        pending_.push_back(pd);
+        return;
     }
-    int64_t bases = 0;
-    for (int32_t i = 0; i < n; ++i) bases += ns_len(seqs[i]);
     const void *const *ptrs = reinterpret_cast<const void *const *>(seqs);
     const bsq_opts o = (opts ? *opts : *options).c_abi();
     uint64_t &calls = bsq_backend_lrand48_calls();
     if (devices_.size() > 1) {   // the fetch spread over the group, member k taking a contiguous share
         ensure_group();
         check(bsq_group_run(group_, &o, ptrs, n, calls));
-        rows_.view_ = bsq_group_hits(group_);
+        group_rows_ = BwaRows();
+        group_rows_.view_ = bsq_group_hits(group_);
+        if (!group_rows_.view_) throw BsqFailure(BSQ_E_NOMEM, bsq_last_error());
+        if (nuclseq_columns && group_rows_.view_->n_hits > 0) {   // rendered now: the reads go away on return
+            uint8_t *cols = nullptr;
+            int64_t *off = nullptr;
+            check(bsq_group_render_nuclseqs(group_, ptrs, &cols, &off));
+            group_rows_.own_cols_.reset(cols);
+            group_rows_.own_off_.reset(off);
+            group_rows_.cols_ = cols;
+            group_rows_.col_off_ = off;
+        }
     } else {
-        ensure_batch(n, bases);
-        check(bsq_batch_set_nuclseqs(batch_, ptrs, n));
-        check(bsq_batch_run(batch_, &o, calls));
-        rows_.view_ = bsq_batch_hits(batch_);
+        ensure_pipe();
+        check(bsq_pipeline_submit(pipe_, &o, ptrs, n, calls, nuclseq_columns ? 1 : 0));
+        ++in_pipe_;
     }
     calls += (uint64_t)n;
-    if (nuclseq_columns && rows_.view_->n_hits > 0) {
-        uint8_t *cols = nullptr;
-        int64_t *off = nullptr;
-        check(group_ ? bsq_group_render_nuclseqs(group_, ptrs, &cols, &off)
-                     : bsq_batch_render_nuclseqs(batch_, ptrs, &cols, &off));
-        rows_.cols_.reset(cols);
-        rows_.col_off_.reset(off);
+    pending_.push_back(pd);
+}
+
+const BwaRows &BwaIndex::take_rows() const
+{
+    if (held_) throw BsqFailure(BSQ_E_INVALID, "release the taken rows first");
+    if (pending_.empty()) throw BsqFailure(BSQ_E_INVALID, "no submitted fetch to take");
+    const Pending pd = pending_.front();
+    pending_.pop_front();
+    rows_ = BwaRows();
+    if (pd.empty) {
+        zeros_.assign((size_t)pd.n + 1, 0);
+        none_ = kNoHits;
+        none_.n_reads = pd.n;
+        none_.read_off = zeros_.data();
+        rows_.view_ = &none_;
+        held_ = 1;
+        held_pipe_ = false;
+        return rows_;
     }
+    if (devices_.size() > 1) {
+        rows_ = std::move(group_rows_);
+        group_rows_ = BwaRows();
+        held_ = 1;
+        held_pipe_ = false;
+        return rows_;
+    }
+    const bsq_hits *v = nullptr;
+    const uint8_t *cols = nullptr;
+    const int64_t *off = nullptr;
+    const int rc = bsq_pipeline_next(pipe_, &v, &cols, &off);
+    if (rc != BSQ_OK) {   // a failed submission has freed its slot
+        --in_pipe_;
+        throw BsqFailure(rc, bsq_last_error());
+    }
+    rows_.view_ = v;
+    rows_.cols_ = pd.cols ? cols : nullptr;
+    rows_.col_off_ = pd.cols ? off : nullptr;
+    held_ = 1;
+    held_pipe_ = true;
     return rows_;
+}
+
+void BwaIndex::release_rows() const
+{
+    if (!held_) return;
+    rows_ = BwaRows();
+    if (held_pipe_) {
+        bsq_pipeline_release(pipe_);
+        --in_pipe_;
+    }
+    held_ = 0;
+    held_pipe_ = false;
+}
+
+void BwaIndex::reset_rows() const
+{
+    release_rows();
+    while (!pending_.empty()) {
+        try {
+            take_rows();
+        } catch (const BsqFailure &) {   // a failed submission: nothing to release
+            continue;
+        }
+        release_rows();
+    }
+}
+
+const BwaRows &BwaIndex::align_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
+                                    const BsqMemOpt *opts) const
+{
+    std::lock_guard<std::mutex> lk(mu_);
+    reset_rows();   // the previous call's rows are released here (they were valid until this call)
+    submit_rows(seqs, n, nuclseq_columns, opts);
+    return take_rows();
 }
 
 std::vector<std::vector<BwaMatch>> BwaIndex::align_sequences(const std::vector<const NucleotideSequence *> &seqs) const

@@ -5,6 +5,9 @@
 //   * BwaIndex::align_rows()      one GPU call for a whole SPI fetch: numeric records, CIGAR ops and the two
 //                                 nuclseq columns of every bwa_result row (build_tuple_bwa's two
 //                                 nuclseq_from_text calls, extension.cpp:285,290, rendered on the GPU);
+//   * submit_rows/take_rows       the same as a pipeline (bsq_pipeline): a fetch is staged and released at
+//                                 once, up to pipeline_depth() fetches align on the device while the backend
+//                                 fetches the next rows and builds the previous fetch's tuples;
 //   * explicit per-call options   a cached index serves calls with different bwa_options;
 //   * BwaIndexCache               the index of a reference cursor kept across calls (the reference rebuilds
 //                                 it on every call, Q13: extension.cpp:326,359), keyed by a digest of the
@@ -71,15 +74,17 @@ public:
     // cigar_compressed_to_string (bwa.cpp:70-77) with htslib's "MIDNSHP=XB" letters (Q8)
     void cigar_text(int64_t k, std::string &out) const;
     // nuclseq varlenas of ref_subseq / query_subseq (nullptr unless align_rows asked for the columns)
-    const void *ref_subseq(int64_t k) const { return cols_ ? cols_.get() + col_off_.get()[2 * k] : nullptr; }
-    const void *query_subseq(int64_t k) const { return cols_ ? cols_.get() + col_off_.get()[2 * k + 1] : nullptr; }
+    const void *ref_subseq(int64_t k) const { return cols_ ? cols_ + col_off_[2 * k] : nullptr; }
+    const void *query_subseq(int64_t k) const { return cols_ ? cols_ + col_off_[2 * k + 1] : nullptr; }
 
 private:
     friend class BwaIndex;
     struct Free { void operator()(void *p) const { bsq_free(p); } };
     const bsq_hits *view_ = nullptr;
-    std::unique_ptr<uint8_t, Free> cols_;
-    std::unique_ptr<int64_t, Free> col_off_;
+    const uint8_t *cols_ = nullptr;             // borrowed from the pipeline slot, or owned below
+    const int64_t *col_off_ = nullptr;
+    std::unique_ptr<uint8_t, Free> own_cols_;   // columns rendered over a device group
+    std::unique_ptr<int64_t, Free> own_off_;
 };
 
 class BwaIndex {
@@ -103,6 +108,19 @@ public:
     const BwaRows &align_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
                               const BsqMemOpt *opts = nullptr) const;
 
+    // Pipelined align_rows for a cursor (bsq_pipeline on one device; a device group runs each fetch at submit):
+    // submit_rows copies the fetch, so its tuples may be released on return, and starts it on the device;
+    // take_rows waits for the oldest submitted fetch and lends its rows until release_rows.  At most
+    // pipeline_depth() fetches may be submitted and not released.  Rows come back in submission order, with
+    // lrand48 positions as if aligned one after another.  Not for concurrent use by several threads.
+    void submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
+                     const BsqMemOpt *opts = nullptr) const;
+    const BwaRows &take_rows() const;
+    void release_rows() const;
+    int pipeline_depth() const;
+    // Releases the taken rows and discards submissions nobody took (e.g. left by a call that failed midway).
+    void reset_rows() const;
+
     bool empty() const;          // no reference bases: align_* return no rows and draw no lrand48 value
     int32_t n_refs() const;
     int device() const { return devices_[0]; }
@@ -111,16 +129,23 @@ public:
     BsqMemOpt *options;          // bwa.h:41 (mem_opt_t* there)
 
 private:
-    void ensure_batch(int32_t n, int64_t bases) const;
+    void ensure_pipe() const;
     void ensure_group() const;
     bsq_index *index_;
     std::vector<int> devices_;
     mutable bsq_group *group_ = nullptr;
-    mutable bsq_batch *batch_ = nullptr;
-    mutable int32_t batch_reads_ = 0;
-    mutable int64_t batch_bases_ = 0;
+    mutable bsq_pipeline *pipe_ = nullptr;
+    struct Pending { bool cols = false, empty = false; int32_t n = 0; };
+    mutable std::list<Pending> pending_;   // submitted, not yet taken (group / empty fetches run at submit)
+    mutable int held_ = 0;                 // taken, not yet released (0 or 1)
+    mutable bool held_pipe_ = false;       // ... and it occupies a slot of pipe_
+    mutable BwaRows group_rows_;           // rows of the pending group fetch (aligned and rendered at submit)
+    mutable int in_pipe_ = 0;              // submissions inside pipe_ not yet released
+    mutable bool group_ready_ = false;     // the group holds the rows of the one pending group fetch
+    mutable std::vector<int64_t> zeros_;   // read offsets of an empty fetch
+    mutable bsq_hits none_{};
     mutable BwaRows rows_;
-    mutable std::mutex mu_;      // one batch per index: calls on a shared (cached) index are serialised
+    mutable std::mutex mu_;      // align_rows on a shared (cached) index is serialised
 };
 
 // Position of this backend in the process-global lrand48 stream (Q10); every aligned read consumes one value,

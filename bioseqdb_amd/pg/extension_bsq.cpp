@@ -30,6 +30,7 @@ extern "C" {
 
 #include <algorithm>
 #include <chrono>
+#include <list>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -381,15 +382,31 @@ void multi_search(FunctionCallInfo fcinfo)
     const CallIndex ci = index_from_query(reference_sql, opts, nuclseq_oid);
     Tuplestorestate *store = create_store(rsi, desc);
     CallStats st;
+    // The cursor loop as a pipeline (bsq_pipeline): each fetch is staged and submitted, its tuples released at
+    // once, and the oldest fetch's rows go into the tuplestore only when the pipeline is full -- so the GPU
+    // aligns fetches k-depth+1..k while the backend fetches k+1 and builds the tuples of k-depth.  Rows still
+    // come out in cursor order (extension.cpp:362-370 aligns and stores one row at a time).
+    const BwaIndex &index = *ci.index;
+    index.reset_rows();   // a cached index may hold submissions of a call that failed midway
+    const int depth = index.pipeline_depth();
+    std::list<std::vector<int64_t>> ids_q;   // query ids of the submitted fetches, oldest first
+    const auto t0 = std::chrono::steady_clock::now();
+    auto drain_one = [&] {
+        const BwaRows &rows = index.take_rows();
+        put_rows(store, desc, rows, ids_q.front().data());
+        st.rows += rows.n_rows();
+        index.release_rows();
+        ids_q.pop_front();
+    };
     for_each_fetch(query_sql, nuclseq_oid, query_fetch_rows(),
                    [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
-                       const auto t0 = std::chrono::steady_clock::now();
-                       const BwaRows &rows = ci.index->align_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt);
-                       put_rows(store, desc, rows, ids.data());
-                       st.align_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                       if ((int)ids_q.size() >= depth) drain_one();
+                       index.submit_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt);
+                       ids_q.push_back(ids);
                        st.reads += (long long)seqs.size();
-                       st.rows += rows.n_rows();
                    });
+    while (!ids_q.empty()) drain_one();
+    st.align_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     finish(rsi, store, desc, "nuclseq_multi_search_bwa", ci, st);
 }
 

@@ -178,14 +178,42 @@ int bsq_group_replicate(bsq_group *g, bsq_index *idx, double *broadcast_ms);
 /* Aligns n_reads nuclseq reads over the members: member k takes reads [k*n/G, (k+1)*n/G) with lrand48
  * positions from first_call_seq + its first read (identical rows to one device aligning all reads in
  * order, Q10/Q16).  Every member runs on its own host thread and copies its records to the host over its
- * own PCIe link; the merged view (read order, batch-wide read_index and cigar_off) is borrowed until the
- * next run or free.  With reads == NULL the members re-run the reads staged by the previous call. */
+ * own PCIe link (pinned memory, one segment per share); the merged view (read order, call-wide read_index and
+ * cigar_off) is borrowed until the next run or free.  With reads == NULL the members re-run the reads staged
+ * (and still resident on their devices) from the previous call. */
 int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
                   uint64_t first_call_seq);
+/* Concurrent shares per member (1..16, default 4): each member splits its shard into up to this many batches
+ * of >= 32768 reads that run at once on its device (a bsq_pipeline).  Set before bsq_group_replicate. */
+int bsq_group_set_slots(bsq_group *g, int slots);
+/* The merged view of the last run (built on first call after a run; NULL on allocation failure). */
 const bsq_hits *bsq_group_hits(const bsq_group *g);
+/* The last run's records without the merge: segment i (one per member share, in read order) covers reads
+ * [read_lo[i], read_lo[i] + views[i]->n_reads) with segment-local read_index / cigar_off.  Writes up to `max`
+ * entries and returns the number of segments.  Borrowed until the next run or free. */
+int bsq_group_segments(const bsq_group *g, const bsq_hits **views, int32_t *read_lo, int max);
 /* build_tuple_bwa's two nuclseq columns of the last run's rows, rendered on every member for its shard
  * (layout as bsq_batch_render_nuclseqs, rows in the merged order).  `reads` as given to bsq_group_run. */
 int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads, uint8_t **out, int64_t **out_off);
+
+/* ---- Pipelined cursor fetches (replaces the fetch-align-materialise loop of
+ * nuclseq_multi_search_bwa, extension.cpp:156-195 + 362-370, which leaves the device idle between fetches).
+ * A pipeline owns n_slots batches on the index's device, each with its own HIP stream and host worker.
+ * bsq_pipeline_submit copies the fetch's nuclseq varlenas (they may be released when it returns) and starts
+ * upload, alignment, the record D2H and, with nuclseq_columns != 0, build_tuple_bwa's two nuclseq columns
+ * per row (as bsq_batch_render_nuclseqs) on the next slot; read i draws lrand48 value first_call_seq + i.
+ * bsq_pipeline_next waits for the oldest submission not yet taken and lends its rows (and columns, NULL when
+ * not asked for or no rows) until bsq_pipeline_release, which frees the oldest taken slot.  At most n_slots
+ * submissions may be submitted and not released: a further submit fails with BSQ_E_INVALID.  A failed
+ * submission reports its error from bsq_pipeline_next and frees its slot. */
+typedef struct bsq_pipeline bsq_pipeline;
+int bsq_pipeline_create(bsq_index *idx, int n_slots, bsq_pipeline **out);
+void bsq_pipeline_free(bsq_pipeline *p);
+int bsq_pipeline_slots(const bsq_pipeline *p);
+int bsq_pipeline_submit(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                        uint64_t first_call_seq, int nuclseq_columns);
+int bsq_pipeline_next(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off);
+int bsq_pipeline_release(bsq_pipeline *p);
 
 /* ---- alignment --------------------------------------------------------------------------------- */
 /* Value of the (pos+1)-th lrand48() call of an unseeded glibc/musl process (Q10). */

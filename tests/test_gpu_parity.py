@@ -122,8 +122,9 @@ def test_parity_smem_list_spill(monkeypatch):
 
 
 def test_parity_wide_rows(monkeypatch):
-    """The 64-bit-row code path of the 3 Gbp configs (u64 SA, 128-base occ blocks, no k-mer table, u64
-    SMEM lists with global spill), forced on a small reference."""
+    """The 64-bit-row code path of the 3 Gbp configs (u64 SA, u64 SMEM lists with global spill, the u64
+    seeding kernel), forced on a small reference.  The k-mer table is built here too (K = 10 at this
+    size, kmer_depth in bsq_api.cpp); the real 3 Gbp index is tested in test_gpu_c4.py."""
     monkeypatch.setenv("BSQ_FORCE_WIDE", "1")
     ref = synth.make_reference(1_000_000, n_rows=3, n_run_every=300_000, n_run_len=400)
     reads = synth.make_reads(ref, 3000, seed=31)
