@@ -826,20 +826,85 @@ def main() -> int:
         t1 = time.perf_counter()
         N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
         dt_s = time.perf_counter() - t1
-        L.bsq_hits_free(ho)
-        ho = ctypes.POINTER(N.Hits)()
-        t1 = time.perf_counter()   # a second call reuses the index's pooled batch (workspace kept)
-        N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
-        dt_s2 = time.perf_counter() - t1
+        dts = []
+        for _ in range(3):   # later calls reuse the index's pipeline (workspaces kept) and result arrays
+            L.bsq_hits_free(ho)
+            ho = ctypes.POINTER(N.Hits)()
+            t1 = time.perf_counter()
+            N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
+            dts.append(time.perf_counter() - t1)
+        dt_s2 = sorted(dts)[1]
         result["sql_batch_call"] = {
             "reads": reads.n, "seconds": round(dt_s, 3), "reads_per_s": round(reads.n / dt_s, 1),
-            "second_call_s": round(dt_s2, 3), "second_call_reads_per_s": round(reads.n / dt_s2, 1),
+            "repeat_call_s": [round(x, 4) for x in dts], "repeat_call_reads_per_s": round(reads.n / dt_s2, 1),
             "same_rows": int(ho.contents.n_hits) == n_hits,
-            "note": "bsq_align_batch from nuclseq varlenas in host memory, one call (allocation, upload, device "
-                    "nt4 conversion, alignment, D2H of the records); the timed metric excludes set-up"}
-        # beside the headline: the same reads through the SQL-level call, PCIe legs included
-        result["value_sql_call"] = round(reads.n / dt_s2, 1)
+            "note": "bsq_align_batch from nuclseq varlenas in host memory, one call (staging, upload, device nt4 "
+                    "conversion, alignment as concurrent shares, D2H, merged result arrays); first call includes "
+                    "workspace allocation; repeat = median of 3"}
         L.bsq_hits_free(ho)
+
+        # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
+        # (262144) reads submitted to a bsq_pipeline of depth 3 (each fetch staged, then its tuples released),
+        # the oldest fetch's rows taken when the pipeline is full; with the two nuclseq columns per row
+        # (build_tuple_bwa) rendered on the GPU, and without them
+        hb.phase = "pipelined cursor fetches"
+        fetch, depth, passes = 262144, 4, 4   # a 4M-read cursor: the batch's reads 4 times (16 fetches)
+
+        t_sub, sub_s = [0.0], [0.0]
+
+        def cursor(cols):
+            p = ctypes.c_void_p()
+            N.check(L.bsq_pipeline_create(idx, depth, ctypes.byref(p)))
+            try:
+                rows, best = 0, None
+                for rep in range(3):   # first pass allocates the slots' workspaces
+                    t_sub[0] = 0.0
+                    t1 = time.perf_counter()
+                    pend, rows = 0, 0
+
+                    def take():
+                        v = ctypes.POINTER(N.Hits)()
+                        N.check(L.bsq_pipeline_next(p, ctypes.byref(v), None, None))
+                        N.check(L.bsq_pipeline_release(p))
+                        return int(v.contents.n_hits)
+                    for lo in [q * reads.n + x for q in range(passes) for x in range(0, reads.n, fetch)]:
+                        if pend == depth:
+                            rows += take()
+                            pend -= 1
+                        r0 = lo % reads.n
+                        n = min(fetch, reads.n - r0)
+                        sp = ctypes.cast(ctypes.addressof(ptrs) + r0 * ctypes.sizeof(ctypes.c_void_p), ctypes.c_void_p)
+                        t2 = time.perf_counter()
+                        N.check(L.bsq_pipeline_submit(p, ctypes.byref(opts), sp, n, first_call + lo, cols))
+                        t_sub[0] += time.perf_counter() - t2
+                        pend += 1
+                    while pend:
+                        rows += take()
+                        pend -= 1
+                    dt = time.perf_counter() - t1
+                    if rep > 0 and (best is None or dt < best):
+                        best = dt
+                        sub_s[0] = t_sub[0]
+                return rows, best
+            finally:
+                L.bsq_pipeline_free(p)
+
+        rows_c, dt_c = cursor(1)
+        sub_c = sub_s[0]
+        rows_r, dt_r = cursor(0)
+        sub_r = sub_s[0]
+        nr = passes * reads.n
+        result["sql_cursor"] = {
+            "reads": nr, "fetch_rows": fetch, "depth": depth,
+            "reads_per_s_with_columns": round(nr / dt_c, 1), "reads_per_s_records_only": round(nr / dt_r, 1),
+            "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits,
+            "submit_s": [round(sub_c, 4), round(sub_r, 4)], "loop_s": [round(dt_c, 4), round(dt_r, 4)],
+            "note": "bsq_pipeline over fetches of host nuclseq varlenas (staging on the caller's thread, upload, "
+                    "alignment, D2H, and with columns the two nuclseq columns of every row on the GPU), as "
+                    "extension_bsq.cpp's cursor loop runs it, over a cursor of the batch's reads 4 times (lrand48 "
+                    "positions continuing); best of 2 runs after a warm-up run"}
+        # beside the headline: the drop-in's own call path (the pipelined cursor loop, columns included)
+        result["value_sql_call"] = round(nr / dt_c, 1)
         del keep, ptrs
 
     # ---- bulk codec: the reference rows through nuclseq_in on the GPU vs the

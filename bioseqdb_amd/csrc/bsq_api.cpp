@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <queue>
 #include <string>
 #include <thread>
@@ -118,6 +119,33 @@ static void set_err(const char *fmt, ...)
         }                                                                                          \
     } while (0)
 
+// Grow-only device scratch of a batch's renderers: chunks allocated once and carved again on every call, so a
+// steady cursor loop never calls hipMalloc/hipFree (hipFree synchronises the whole device, stalling every other
+// batch's stream).  reset() at the start of a call; the chunks are freed with the batch.
+struct DevArena {
+    std::vector<std::pair<void *, size_t>> chunks;
+    size_t ci = 0, used = 0;
+    void reset() { ci = 0; used = 0; }
+    template <typename T>
+    hipError_t get(T *&out, size_t count)
+    {
+        const size_t bytes = (std::max<size_t>(count, 1) * sizeof(T) + 255) & ~(size_t)255;
+        while (ci < chunks.size() && used + bytes > chunks[ci].second) { ++ci; used = 0; }
+        if (ci == chunks.size()) {
+            void *q = nullptr;
+            const size_t cap = std::max<size_t>(bytes, (size_t)64 << 20);
+            const hipError_t e = hipMalloc(&q, cap);
+            if (e != hipSuccess) return e;
+            chunks.emplace_back(q, cap);
+            used = 0;
+        }
+        out = reinterpret_cast<T *>(static_cast<uint8_t *>(chunks[ci].first) + used);
+        used += bytes;
+        return hipSuccess;
+    }
+    ~DevArena() { for (auto &c : chunks) hipFree(c.first); }
+};
+
 extern "C" const char *bsq_last_error(void) { return g_err.c_str(); }
 // for the other translation units of the library (group.cpp); not part of include/bsq.h
 extern "C" void bsq_internal_set_error(const char *msg) { g_err = msg ? msg : ""; }
@@ -182,6 +210,10 @@ extern "C" void bsq_index_free(bsq_index *idx)
 {
     if (!idx) return;
     bsq_pipeline_free(idx->pipe);
+    if (idx->d_rh) {
+        if (idx->h.dev) hipSetDevice(idx->h.dev->device);
+        hipFree(idx->d_rh);
+    }
     delete idx->h.dev;
     delete idx;
 }
@@ -839,6 +871,11 @@ struct bsq_batch {
     int64_t r_hits_cap = 0, r_cig_cap = 0, r_len_cap = 0, r_text_cap = 0;
     char *r_host = nullptr; int64_t r_host_cap = 0;
     void *r_tmp = nullptr; size_t r_tmp_bytes = 0;
+    RenderHole *r_qh = nullptr; int64_t r_qh_cap = 0;   // the reads' own hole symbols
+    int64_t *r_qoff = nullptr; int64_t r_qoff_cap = 0;
+    DevArena arena;                                     // encode scratch of the nuclseq columns
+    uint8_t *c_host = nullptr; int64_t c_host_cap = 0;  // the columns' varlenas and offsets (pinned; borrowed out)
+    int64_t *c_off = nullptr; int64_t c_off_cap = 0;
     hipEvent_t ev[STG_N + 1]{};
     float stage_ms[STG_N]{};
     double stage_bytes[STG_N]{};
@@ -942,6 +979,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->ovf_list); hipFree(b->ovf_count); hipFree(b->cub_tmp); hipFree(b->d_out); hipFree(b->d_out_cig);
     hipHostFree(b->h_pinned); hipHostFree(b->h_pinned_cig); hipHostFree(b->h_pinned_off); hipFree(b->d_intv);
     hipFree(b->r_hits); hipFree(b->r_cig); hipFree(b->r_len); hipFree(b->r_text); hipFree(b->r_tmp); hipHostFree(b->r_host);
+    hipFree(b->r_qh); hipFree(b->r_qoff); hipHostFree(b->c_host); hipHostFree(b->c_off);
     hipFree(b->ns_dev); hipFree(b->ns_meta);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
@@ -1016,39 +1054,84 @@ int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
 {
     if (n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
     const size_t n = (size_t)n_reads;
+    // Two passes over contiguous ranges of the reads, on up to 8 host threads for a large fetch (a cursor
+    // fetch of 256k reads is ~13 MB of varlenas): sizes and offsets, then the copy into pinned memory.
+    const int T = n >= 65536 ? (int)std::max<unsigned>(1, std::min<unsigned>(8, std::thread::hardware_concurrency())) : 1;
+    std::vector<size_t> lo((size_t)T + 1);
+    for (int t = 0; t <= T; ++t) lo[(size_t)t] = n * (size_t)t / (size_t)T;
     s.meta.assign(2 * (n + 1), 0);   // in_off | poff, then the holed reads
     s.offs.assign(n + 1, 0);
+    int64_t *in_off = s.meta.data(), *poff = s.meta.data() + n + 1, *boff = s.offs.data();
+    struct Part { int64_t in = 0, pac = 0, bases = 0; int max_len = 0; std::vector<int64_t> holed;
+                  size_t bad = SIZE_MAX; int kind = 0; uint64_t vl = 0, need = 0; };
+    std::vector<Part> part((size_t)T);
+    auto pass1 = [&](int t) {   // per-read sizes at [i] (a range's thread alone touches [lo, hi))
+        Part &q = part[(size_t)t];
+        for (size_t i = lo[(size_t)t]; i < lo[(size_t)t + 1]; ++i) {
+            const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
+            if (!ns) { q.bad = i; q.kind = 1; return; }
+            uint32_t vl; memcpy(&vl, ns, 4);
+            const uint64_t nh = ns_holes_num(ns), len = ns_len(ns), need = 12 + 16 * nh + pac_byte_size(len);
+            if ((vl >> 2) < need) { q.bad = i; q.kind = 2; q.vl = vl >> 2; q.need = need; return; }
+            if (nh) q.holed.push_back((int64_t)i);
+            in_off[i] = (int64_t)((need + 7) & ~7ull);
+            poff[i] = (int64_t)pac_byte_size(len);
+            boff[i] = (int64_t)len;
+            q.in += in_off[i];
+            q.pac += poff[i];
+            q.bases += (int64_t)len;
+            q.max_len = std::max<int>(q.max_len, (int)len);
+        }
+    };
+    auto run = [&](auto f) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(f, t);
+        f(0);
+        for (auto &x : th) x.join();
+    };
+    run(pass1);
+    for (const Part &q : part)
+        if (q.bad != SIZE_MAX) {
+            if (q.kind == 1) set_err("read %zu is NULL", q.bad);
+            else set_err("read %zu: varlena of %llu bytes, %llu needed", q.bad, (unsigned long long)q.vl,
+                         (unsigned long long)q.need);
+            return BSQ_E_INVALID;
+        }
+    std::vector<int64_t> base_in((size_t)T + 1, 0), base_pac((size_t)T + 1, 0), base_b((size_t)T + 1, 0);
     int max_len = 0;
-    for (size_t i = 0; i < n; ++i) {
-        const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
-        if (!ns) { set_err("read %zu is NULL", i); return BSQ_E_INVALID; }
-        uint32_t vl; memcpy(&vl, ns, 4);
-        const uint64_t nh = ns_holes_num(ns), len = ns_len(ns), need = 12 + 16 * nh + pac_byte_size(len);
-        if ((vl >> 2) < need) { set_err("read %zu: varlena of %u bytes, %llu needed", i, vl >> 2, (unsigned long long)need); return BSQ_E_INVALID; }
-        if (nh) s.meta.push_back((int64_t)i);
-        int64_t *in_off = s.meta.data(), *poff = s.meta.data() + n + 1;
-        in_off[i + 1] = in_off[i] + (int64_t)((need + 7) & ~7ull);
-        poff[i + 1] = poff[i] + (int64_t)pac_byte_size(len);
-        s.offs[i + 1] = s.offs[i] + (int64_t)len;
-        max_len = std::max<int>(max_len, (int)len);
+    for (int t = 0; t < T; ++t) {
+        base_in[(size_t)t + 1] = base_in[(size_t)t] + part[(size_t)t].in;
+        base_pac[(size_t)t + 1] = base_pac[(size_t)t] + part[(size_t)t].pac;
+        base_b[(size_t)t + 1] = base_b[(size_t)t] + part[(size_t)t].bases;
+        max_len = std::max(max_len, part[(size_t)t].max_len);
     }
-    const int64_t *in_off = s.meta.data(), *poff = s.meta.data() + n + 1;
-    const int64_t bytes = in_off[n];
+    const int64_t bytes = base_in[(size_t)T];
     if (bytes > s.host_cap) {
         if (s.host) hipHostFree(s.host);
         s.host = nullptr;
         s.host_cap = 0;
-        const int64_t cap = std::max<int64_t>(bytes, 4096);
+        const int64_t cap = std::max<int64_t>(bytes + bytes / 4, 4096);
         if (hipHostMalloc((void **)&s.host, (size_t)cap) != hipSuccess) { s.host = nullptr; set_err("out of pinned host memory"); return BSQ_E_NOMEM; }
         s.host_cap = cap;
     }
-    for (size_t i = 0; i < n; ++i) {
-        const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
-        memcpy(s.host + in_off[i], ns, 12 + 16 * (size_t)ns_holes_num(ns) + (size_t)(poff[i + 1] - poff[i]));
-    }
+    auto pass2 = [&](int t) {   // sizes -> offsets within the range, then the copy
+        int64_t a = base_in[(size_t)t], c = base_pac[(size_t)t], d = base_b[(size_t)t];
+        for (size_t i = lo[(size_t)t]; i < lo[(size_t)t + 1]; ++i) {
+            const uint8_t *ns = static_cast<const uint8_t *>(reads[i]);
+            const int64_t ni = in_off[i], pi = poff[i], bi = boff[i];
+            in_off[i] = a; poff[i] = c; boff[i] = d;
+            memcpy(s.host + a, ns, 12 + 16 * (size_t)ns_holes_num(ns) + (size_t)pi);
+            a += ni; c += pi; d += bi;
+        }
+    };
+    run(pass2);
+    in_off[n] = bytes;
+    poff[n] = base_pac[(size_t)T];
+    boff[n] = base_b[(size_t)T];
+    for (const Part &q : part) s.meta.insert(s.meta.end(), q.holed.begin(), q.holed.end());
     s.n = n_reads;
     s.max_len = max_len;
-    s.bases = s.offs[n];
+    s.bases = boff[n];
     s.host_bytes = bytes;
     return BSQ_OK;
 }
@@ -1673,27 +1756,47 @@ static int grow_dev(T *&p, int64_t &cap, int64_t need)
     return BSQ_OK;
 }
 
-// device inputs of the GPU renderers: the last run's records, the reference holes by offset and the reads'
-// own holes (freed with the object)
-struct RenderInputs {
-    RenderView v{};
-    void *p[3] = {nullptr, nullptr, nullptr};
-    ~RenderInputs() { for (void *q : p) if (q) hipFree(q); }
-};
+// The reference's hole overlay as disjoint segments (bsq_index.h HoleIndex, shared with the host renderer), in
+// HBM of the index's device: uploaded on first use, kept with the index.
+static int index_render_holes(bsq_index *idx, const RenderHole **d, int64_t *n)
+{
+    std::lock_guard<std::mutex> lk(idx->rh_mu);
+    if (idx->n_rh < 0) {
+        std::vector<RenderHole> rh;
+        for (const HoleRef &x : idx->holes().segs) rh.push_back(RenderHole{x.beg, x.end, x.order, (uint8_t)x.amb});
+        if (!rh.empty()) {
+            HIPCHK(hipMalloc(&idx->d_rh, rh.size() * sizeof(RenderHole)));
+            HIPCHK(hipMemcpy(idx->d_rh, rh.data(), rh.size() * sizeof(RenderHole), hipMemcpyHostToDevice));
+        }
+        idx->n_rh = (int64_t)rh.size();
+    }
+    *d = static_cast<const RenderHole *>(idx->d_rh);
+    *n = idx->n_rh;
+    return BSQ_OK;
+}
 
-static int render_inputs(bsq_batch *b, const void *const *reads, RenderInputs &ri)
+// Device inputs of the GPU renderers: the last run's records (still in HBM when the run was one chunk without
+// retried reads, else uploaded from the host view), the reference holes, the reads' own holes.  Every buffer is
+// the batch's or the index's (grow-only): nothing is allocated or freed in a steady loop.
+static int render_inputs(bsq_batch *b, const void *const *reads, RenderView &v)
 {
     const bsq_hits &H = b->view;
     hipStream_t st = b->stream;
     const HostIndex &h = b->idx->h;
-    { int rc = grow_dev(b->r_hits, b->r_hits_cap, H.n_hits); if (rc) return rc; }
-    { int rc = grow_dev(b->r_cig, b->r_cig_cap, std::max<int64_t>(H.n_cigar, 1)); if (rc) return rc; }
+    const bsq_hit *dh = b->d_out;
+    const uint32_t *dc = b->d_out_cig;
+    if (!b->dev_whole) {
+        { int rc = grow_dev(b->r_hits, b->r_hits_cap, H.n_hits); if (rc) return rc; }
+        { int rc = grow_dev(b->r_cig, b->r_cig_cap, std::max<int64_t>(H.n_cigar, 1)); if (rc) return rc; }
+        HIPCHK(hipMemcpyAsync(b->r_hits, H.hits, (size_t)H.n_hits * sizeof(bsq_hit), hipMemcpyHostToDevice, st));
+        if (H.n_cigar) HIPCHK(hipMemcpyAsync(b->r_cig, H.cigar, (size_t)H.n_cigar * 4, hipMemcpyHostToDevice, st));
+        dh = b->r_hits;
+        dc = b->r_cig;
+    }
     { int rc = grow_dev(b->r_len, b->r_len_cap, H.n_hits + 1); if (rc) return rc; }
-    HIPCHK(hipMemcpyAsync(b->r_hits, H.hits, (size_t)H.n_hits * sizeof(bsq_hit), hipMemcpyHostToDevice, st));
-    if (H.n_cigar) HIPCHK(hipMemcpyAsync(b->r_cig, H.cigar, (size_t)H.n_cigar * 4, hipMemcpyHostToDevice, st));
-    // the reference's hole overlay as disjoint segments (bsq_index.h HoleIndex, shared with the host renderer)
-    std::vector<RenderHole> rh;
-    for (const HoleRef &x : b->idx->holes().segs) rh.push_back(RenderHole{x.beg, x.end, x.order, (uint8_t)x.amb});
+    const RenderHole *d_rh = nullptr;
+    int64_t n_rh = 0;
+    { const int rc = index_render_holes(b->idx, &d_rh, &n_rh); if (rc) return rc; }
     // the reads' own hole symbols (nuclseq varlenas); without them, ambiguous bases print as N
     std::vector<int64_t> qoff;
     std::vector<RenderHole> qh;
@@ -1710,21 +1813,18 @@ static int render_inputs(bsq_batch *b, const void *const *reads, RenderInputs &r
         }
         if (qh.empty()) qoff.clear();
     }
-    RenderHole *d_rh = nullptr, *d_qh = nullptr;
-    int64_t *d_qoff = nullptr;
-    void **fr = ri.p;
-    if (!rh.empty()) {
-        HIPCHK(hipMalloc(&d_rh, rh.size() * sizeof(RenderHole))); fr[0] = d_rh;
-        HIPCHK(hipMemcpyAsync(d_rh, rh.data(), rh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
-    }
+    const RenderHole *d_qh = nullptr;
+    const int64_t *d_qoff = nullptr;
     if (!qoff.empty()) {
-        HIPCHK(hipMalloc(&d_qh, qh.size() * sizeof(RenderHole))); fr[1] = d_qh;
-        HIPCHK(hipMalloc(&d_qoff, qoff.size() * 8)); fr[2] = d_qoff;
-        HIPCHK(hipMemcpyAsync(d_qh, qh.data(), qh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(d_qoff, qoff.data(), qoff.size() * 8, hipMemcpyHostToDevice, st));
+        { int rc = grow_dev(b->r_qh, b->r_qh_cap, (int64_t)qh.size()); if (rc) return rc; }
+        { int rc = grow_dev(b->r_qoff, b->r_qoff_cap, (int64_t)qoff.size()); if (rc) return rc; }
+        HIPCHK(hipMemcpyAsync(b->r_qh, qh.data(), qh.size() * sizeof(RenderHole), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->r_qoff, qoff.data(), qoff.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));   // the host vectors go out of scope
+        d_qh = b->r_qh;
+        d_qoff = b->r_qoff;
     }
-    ri.v = RenderView{b->r_hits, b->r_cig, H.n_hits, h.dev->pac, h.l_pac, d_rh, (int64_t)rh.size(), b->codes,
-                      b->offs, d_qoff, d_qh};
+    v = RenderView{dh, dc, H.n_hits, h.dev->pac, h.l_pac, d_rh, n_rh, b->codes, b->offs, d_qoff, d_qh};
     return BSQ_OK;
 }
 
@@ -1736,9 +1836,8 @@ extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const ch
     if (H.n_hits <= 0) return BSQ_OK;
     HIPCHK(hipSetDevice(b->device));
     hipStream_t st = b->stream;
-    RenderInputs ri;
-    { const int rc = render_inputs(b, reads, ri); if (rc) return rc; }
-    const RenderView &v = ri.v;
+    RenderView v{};
+    { const int rc = render_inputs(b, reads, v); if (rc) return rc; }
     HIPCHK(launch_row_len(st, v, b->r_len));
     HIPCHK(hipMemsetAsync(b->r_len + H.n_hits, 0, 8, st));
     size_t tb = 0;
@@ -1796,6 +1895,54 @@ extern "C" int64_t bsq_batch_retried(const bsq_batch *b) { return b ? b->retried
 // ================================================================================================
 // one-shot API
 // ================================================================================================
+// Result arrays of the one-shot call.  A cursor calls bsq_align_batch fetch after fetch with results of similar
+// size, and fresh malloc'd pages of ~90 MB per 1M reads cost more to fault in than the copy into them; freed
+// result arrays are kept (a few, at most 2 GB) and handed to the next call that fits.  Each array carries its
+// capacity in a 64-byte header.
+namespace {
+std::mutex g_out_mu;
+std::vector<std::pair<size_t, void *>> g_out_cache;   // (capacity, header), most recently freed last
+size_t g_out_bytes = 0;
+constexpr size_t kOutCacheBytes = (size_t)2 << 30, kOutCacheN = 6, kOutHdr = 64;
+
+void *out_alloc(size_t bytes)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_out_mu);
+        size_t best = SIZE_MAX;
+        for (size_t i = 0; i < g_out_cache.size(); ++i) {
+            const size_t c = g_out_cache[i].first;
+            if (c >= bytes && c <= 2 * bytes + (1 << 20) && (best == SIZE_MAX || c < g_out_cache[best].first)) best = i;
+        }
+        if (best != SIZE_MAX) {
+            void *hdr = g_out_cache[best].second;
+            g_out_bytes -= g_out_cache[best].first;
+            g_out_cache.erase(g_out_cache.begin() + (long)best);
+            return static_cast<uint8_t *>(hdr) + kOutHdr;
+        }
+    }
+    void *hdr = malloc(bytes + kOutHdr);
+    if (!hdr) return nullptr;
+    *static_cast<size_t *>(hdr) = bytes;
+    return static_cast<uint8_t *>(hdr) + kOutHdr;
+}
+
+void out_free(void *p)
+{
+    if (!p) return;
+    void *hdr = static_cast<uint8_t *>(p) - kOutHdr;
+    const size_t cap = *static_cast<size_t *>(hdr);
+    std::lock_guard<std::mutex> lk(g_out_mu);
+    g_out_cache.emplace_back(cap, hdr);
+    g_out_bytes += cap;
+    while (g_out_cache.size() > kOutCacheN || g_out_bytes > kOutCacheBytes) {
+        g_out_bytes -= g_out_cache.front().first;
+        free(g_out_cache.front().second);
+        g_out_cache.erase(g_out_cache.begin());
+    }
+}
+}  // namespace
+
 extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
                                uint64_t first_call_seq, bsq_hits **out)
 {
@@ -1808,7 +1955,9 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     h->n_reads = n_reads;
     if (!idx->h.built) { free(h); set_err("index not built"); return BSQ_E_INVALID; }
     if (idx->h.seq_len == 0 || n_reads == 0) {   // empty reference: align_sequence returns {} (bwa.cpp:142-143)
-        h->read_off = (int64_t *)calloc((size_t)n_reads + 1, 8);
+        h->read_off = (int64_t *)out_alloc(((size_t)n_reads + 1) * 8);
+        if (!h->read_off) { free(h); set_err("out of host memory"); return BSQ_E_NOMEM; }
+        memset(h->read_off, 0, ((size_t)n_reads + 1) * 8);
         *out = h;
         return BSQ_OK;
     }
@@ -1872,9 +2021,9 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     }
     h->n_hits = hb[(size_t)k];
     h->n_cigar = cb[(size_t)k];
-    h->hits = (bsq_hit *)malloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
-    h->cigar = (uint32_t *)malloc(4 * (size_t)std::max<int64_t>(h->n_cigar, 1));
-    h->read_off = (int64_t *)malloc(8 * ((size_t)n_reads + 1));
+    h->hits = (bsq_hit *)out_alloc(sizeof(bsq_hit) * (size_t)std::max<int64_t>(h->n_hits, 1));
+    h->cigar = (uint32_t *)out_alloc(4 * (size_t)std::max<int64_t>(h->n_cigar, 1));
+    h->read_off = (int64_t *)out_alloc(8 * ((size_t)n_reads + 1));
     if (!h->hits || !h->cigar || !h->read_off) {
         release_all();
         bsq_hits_free(h);
@@ -1908,7 +2057,7 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
 extern "C" void bsq_hits_free(bsq_hits *h)
 {
     if (!h) return;
-    free(h->hits); free(h->cigar); free(h->read_off); free(h);
+    out_free(h->hits); out_free(h->cigar); out_free(h->read_off); free(h);
 }
 
 // ================================================================================================
@@ -1958,7 +2107,8 @@ int codec_device(int device)
 // nuclseq_from_text of n texts already in HBM (text i at d_text + toff[i], pac bytes poff[]): the varlenas
 // are written to *d_out at the device offsets *d_off (n+1, 8-byte aligned), *total bytes.  With validate,
 // a character nuclseq_in rejects stops before the write pass: *first_bad = its text offset (else ~0).
-static int encode_device(hipStream_t st, DevAllocs &da, const uint8_t *d_text, const std::vector<int64_t> &toff,
+template <class Alloc>
+static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const std::vector<int64_t> &toff,
                          const std::vector<int64_t> &poff, int64_t n, bool validate, uint8_t **d_out, int64_t **d_off,
                          int64_t *total, unsigned long long *first_bad, double *kernel_ms)
 {
@@ -2089,10 +2239,11 @@ extern "C" int bsq_nuclseq_encode_batch(int device, const char *text, const int6
 // nuclseq_from_text on ref_subseq and query_subseq per row, :285,290): the subsequence texts are written
 // by the GPU renderer and encoded in place by the bulk codec; varlena 2k = ref_subseq of row k, 2k+1 =
 // its query_subseq.
-extern "C" int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **out, int64_t **out_off)
+// build_tuple_bwa's two nuclseq columns of the last run's rows into the batch's pinned buffers (borrowed until the
+// next render or run of the batch): rows' texts rendered in HBM, encoded in place by the bulk codec, one D2H.
+namespace bsq {
+int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **out, const int64_t **out_off)
 {
-    if (!b || !out || !out_off) { set_err("invalid argument"); return BSQ_E_INVALID; }
-    *out = nullptr; *out_off = nullptr;
     const double t_call = now_ms();
     const bsq_hits &H = b->view;
     const int64_t n = 2 * H.n_hits;
@@ -2108,27 +2259,52 @@ extern "C" int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads,
             poff[i + 1] = poff[i] + (l[t] + 3) / 4;
         }
     }
-    DevAllocs da;
+    b->arena.reset();
     char *d_text;
     int64_t *d_toff;
-    HIPCHK(da.get(d_text, (size_t)toff[(size_t)n]));
-    HIPCHK(da.get(d_toff, (size_t)n + 1));
-    RenderInputs ri;
+    HIPCHK(b->arena.get(d_text, (size_t)toff[(size_t)n]));
+    HIPCHK(b->arena.get(d_toff, (size_t)n + 1));
     if (H.n_hits) {
-        { const int rc = render_inputs(b, reads, ri); if (rc) return rc; }
+        RenderView v{};
+        { const int rc = render_inputs(b, reads, v); if (rc) return rc; }
         HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(launch_sub_write(st, ri.v, d_toff, d_text));
+        HIPCHK(launch_sub_write(st, v, d_toff, d_text));
     }
     uint8_t *d_out = nullptr;
     int64_t *d_off = nullptr, total = 0;
     unsigned long long first_bad = ~0ull;
     double kms = 0;
-    { const int rc = encode_device(st, da, reinterpret_cast<const uint8_t *>(d_text), toff, poff, n, false, &d_out, &d_off,
-                                   &total, &first_bad, &kms);
+    { const int rc = encode_device(st, b->arena, reinterpret_cast<const uint8_t *>(d_text), toff, poff, n, false, &d_out,
+                                   &d_off, &total, &first_bad, &kms);
       if (rc) return rc; }
-    { const int rc = download(st, d_out, d_off, n, total, out, out_off); if (rc) return rc; }
+    { int rc = grow_pinned(b->c_host, b->c_host_cap, std::max<int64_t>(total, 1), 0); if (rc) return rc; }
+    { int rc = grow_pinned(b->c_off, b->c_off_cap, n + 1, 0); if (rc) return rc; }
+    if (total) HIPCHK(hipMemcpyAsync(b->c_host, d_out, (size_t)total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->c_off, d_off, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *out = b->c_host;
+    *out_off = b->c_off;
     g_codec_ms[0] = kms;
     g_codec_ms[1] = now_ms() - t_call;
+    return BSQ_OK;
+}
+}  // namespace bsq
+
+extern "C" int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **out, int64_t **out_off)
+{
+    if (!b || !out || !out_off) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    *out = nullptr; *out_off = nullptr;
+    const uint8_t *c = nullptr;
+    const int64_t *o = nullptr;
+    { const int rc = batch_render_cols(b, reads, &c, &o); if (rc) return rc; }
+    const int64_t n = 2 * b->view.n_hits, total = o[n];
+    uint8_t *h_buf = static_cast<uint8_t *>(malloc((size_t)std::max<int64_t>(total, 1)));
+    int64_t *h_off = static_cast<int64_t *>(malloc(((size_t)n + 1) * 8));
+    if (!h_buf || !h_off) { free(h_buf); free(h_off); set_err("out of host memory"); return BSQ_E_NOMEM; }
+    if (total) memcpy(h_buf, c, (size_t)total);
+    memcpy(h_off, o, ((size_t)n + 1) * 8);
+    *out = h_buf;
+    *out_off = h_off;
     return BSQ_OK;
 }
 

@@ -99,6 +99,10 @@ struct bsq_index {
     bsq::HostIndex h;
     std::mutex pool_mu;
     bsq_pipeline *pipe = nullptr;
+    // the reference holes as render segments in HBM (bsq_api.cpp index_render_holes), uploaded on first use
+    std::mutex rh_mu;
+    void *d_rh = nullptr;
+    int64_t n_rh = -1;
     // offset-ordered holes for host rendering, built on first use after the index is built
     std::once_flag hx_once;
     std::unique_ptr<bsq::HoleIndex> hx;

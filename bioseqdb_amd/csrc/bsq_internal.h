@@ -36,6 +36,9 @@ int32_t batch_max_reads(const bsq_batch *b);
 int64_t batch_max_bases(const bsq_batch *b);
 
 void set_error(const std::string &msg);
+// bsq_batch_render_nuclseqs into the batch's own pinned buffers: *out / *out_off are borrowed until the next
+// render or run of the batch (the pipeline hands them out until the slot is released).
+int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **out, const int64_t **out_off);
 
 // pipeline.cpp: how a submission's reads reach the slot.  COPY: staged on the caller's thread before submit
 // returns (the public bsq_pipeline_submit).  DEFER: staged by the slot's worker (the reads must stay valid

@@ -54,8 +54,8 @@ struct Slot {
     const bsq_hits *view = nullptr;
     bsq_hits empty{};
     std::vector<int64_t> zeros;
-    uint8_t *col_buf = nullptr;
-    int64_t *col_off = nullptr;
+    const uint8_t *col_buf = nullptr;     // the batch's pinned column buffers (borrowed)
+    const int64_t *col_off = nullptr;
     std::thread th;
 };
 
@@ -74,8 +74,6 @@ namespace {
 
 void drop_cols(Slot &x)
 {
-    bsq_free(x.col_buf);
-    bsq_free(x.col_off);
     x.col_buf = nullptr;
     x.col_off = nullptr;
 }
@@ -121,7 +119,7 @@ int run_job(bsq_pipeline *p, Slot &x)
         // the staged varlenas carry the reads' hole symbols (the caller's may be gone)
         std::vector<const void *> ptrs((size_t)x.n);
         for (int32_t i = 0; i < x.n; ++i) ptrs[(size_t)i] = x.stage.host + x.stage.meta[(size_t)i];
-        const int rc = bsq_batch_render_nuclseqs(x.batch, ptrs.data(), &x.col_buf, &x.col_off);
+        const int rc = batch_render_cols(x.batch, ptrs.data(), &x.col_buf, &x.col_off);
         if (rc) return rc;
     }
     return BSQ_OK;

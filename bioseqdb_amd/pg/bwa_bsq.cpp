@@ -98,7 +98,7 @@ int BwaIndex::pipeline_depth() const
 {
     if (devices_.size() > 1) return 1;   // a group aligns its fetch at submit (every member pipelines its shard)
     const char *e = getenv("BSQ_PIPE_DEPTH");
-    const int d = e ? atoi(e) : 3;
+    const int d = e ? atoi(e) : 4;   // 4 fetches on the device at once (bench.py sql_cursor)
     return std::max(1, std::min(d, 16));
 }
 

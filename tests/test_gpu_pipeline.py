@@ -157,3 +157,30 @@ def test_one_shot_split_does_not_change_rows(setup, monkeypatch):
     monkeypatch.setenv("BSQ_PIPE_SLOTS", "4")
     b = _one_shot(L, pi.handle, pi.options, big, 42)
     assert a == b
+
+
+def test_large_fetch_threaded_staging(setup):
+    """A fetch of >= 65536 reads is staged on several host threads (stage_nuclseqs); its rows and columns must
+    equal the same reads aligned as three one-shot shares (each staged on one thread)."""
+    pi, seqs = setup
+    L = N.lib()
+    big = (seqs * 3)[:70001]
+    holed = sum(1 for s in big if s.holes_num)
+    assert holed > 10   # reads with N exercise the holed-read list of the staging
+    p = ctypes.c_void_p()
+    N.check(L.bsq_pipeline_create(pi.handle, 1, ctypes.byref(p)))
+    try:
+        ptrs = (ctypes.c_void_p * len(big))(*[s.ptr for s in big])
+        N.check(L.bsq_pipeline_submit(p, ctypes.byref(pi.options), ptrs, len(big), 7, 1))
+        v = ctypes.POINTER(N.Hits)()
+        c = ctypes.c_void_p()
+        o = ctypes.POINTER(ctypes.c_int64)()
+        N.check(L.bsq_pipeline_next(p, ctypes.byref(v), ctypes.byref(c), ctypes.byref(o)))
+        got = _records(v.contents, len(big))
+        nh = v.contents.n_hits
+        cols = ctypes.string_at(c, o[2 * nh])
+        N.check(L.bsq_pipeline_release(p))
+    finally:
+        L.bsq_pipeline_free(p)
+    assert got == _one_shot(L, pi.handle, pi.options, big, 7)
+    assert cols == _columns(L, pi.handle, pi.options, big, 7)
