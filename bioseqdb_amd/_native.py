@@ -79,6 +79,7 @@ SIGNATURES = {
     "bsq_index_seq_len": (ctypes.c_int64, [_P]),
     "bsq_index_primary": (ctypes.c_int64, [_P]),
     "bsq_index_n_refs": (ctypes.c_int32, [_P]),
+    "bsq_index_same_refs": (ctypes.c_int, [_P, _P]),
     "bsq_index_sa": (ctypes.c_int64, [_P, ctypes.c_int64]),
     "bsq_index_occ4": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]),
     "bsq_index_sa_data": (_P, [_P, ctypes.POINTER(ctypes.c_int)]),

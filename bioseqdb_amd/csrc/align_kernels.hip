@@ -359,15 +359,17 @@ struct ChainNode { int64_t pos; int32_t rid, n, head, tail, w, kept, first, pad;
 struct KNode { int32_t n, is_internal; int32_t key[9]; int32_t ptr[10]; };
 #define KB_T 5
 
+template <int S>
 struct ChainCtx {
-    SP<SeedNode> seeds; int n_seeds, cap_seeds;
-    SP<ChainNode> ch; int n_ch, cap_ch;
-    SP<KNode> nodes; int n_nodes, cap_nodes;
+    SP<SeedNode, S> seeds; int n_seeds, cap_seeds;
+    SP<ChainNode, S> ch; int n_ch, cap_ch;
+    SP<KNode, S> nodes; int n_nodes, cap_nodes;
     int root, n_keys;
     bool ovf;
 };
 
-DEV int kb_getp_aux(const ChainCtx &C, const KNode &x, int64_t kpos, int *r)
+template <int S>
+DEV int kb_getp_aux(const ChainCtx<S> &C, const KNode &x, int64_t kpos, int *r)
 {
     int tr, *rr = r ? r : &tr, begin = 0, end = x.n;
     if (x.n == 0) return -1;
@@ -382,7 +384,8 @@ DEV int kb_getp_aux(const ChainCtx &C, const KNode &x, int64_t kpos, int *r)
     return begin;
 }
 
-DEV int kb_intervalp_lower(const ChainCtx &C, int64_t kpos)
+template <int S>
+DEV int kb_intervalp_lower(const ChainCtx<S> &C, int64_t kpos)
 {
     int i, r = 0, x = C.root, lower = -1;
     while (x >= 0) {
@@ -396,7 +399,8 @@ DEV int kb_intervalp_lower(const ChainCtx &C, int64_t kpos)
     return lower;
 }
 
-DEV int kb_new_node(ChainCtx &C)
+template <int S>
+DEV int kb_new_node(ChainCtx<S> &C)
 {
     if (C.n_nodes >= C.cap_nodes) { C.ovf = true; return -1; }
     KNode &z = C.nodes[C.n_nodes];
@@ -404,7 +408,8 @@ DEV int kb_new_node(ChainCtx &C)
     return C.n_nodes++;
 }
 
-DEV bool kb_split(ChainCtx &C, int xi, int i, int yi)
+template <int S>
+DEV bool kb_split(ChainCtx<S> &C, int xi, int i, int yi)
 {
     int zi = kb_new_node(C);
     if (zi < 0) return false;
@@ -422,7 +427,8 @@ DEV bool kb_split(ChainCtx &C, int xi, int i, int yi)
     return true;
 }
 
-DEV void kb_putp(ChainCtx &C, int key)
+template <int S>
+DEV void kb_putp(ChainCtx<S> &C, int key)
 {
     ++C.n_keys;
     int r = C.root;
@@ -455,7 +461,8 @@ DEV void kb_putp(ChainCtx &C, int key)
     }
 }
 
-DEV bool test_and_merge(ChainCtx &C, const DOpts &o, int64_t l_pac, int ci, const SeedNode &p, int seed_rid)
+template <int S>
+DEV bool test_and_merge(ChainCtx<S> &C, const DOpts &o, int64_t l_pac, int ci, const SeedNode &p, int seed_rid)
 {
     ChainNode &c = C.ch[ci];
     const SeedNode &first = C.seeds[c.head], &last = C.seeds[c.tail];
@@ -477,7 +484,8 @@ DEV bool test_and_merge(ChainCtx &C, const DOpts &o, int64_t l_pac, int ci, cons
     return false;
 }
 
-DEV int chain_weight(const ChainCtx &C, const ChainNode &c)
+template <int S>
+DEV int chain_weight(const ChainCtx<S> &C, const ChainNode &c)
 {
     int64_t end = 0;
     int w = 0, tmp;
@@ -498,6 +506,7 @@ DEV int chain_weight(const ChainCtx &C, const ChainNode &c)
     return w < (1 << 30) ? w : (1 << 30) - 1;
 }
 
+template <int S>
 __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, const int64_t *offs, const int32_t *sel,
                                                int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains_out,
                                                Seed *seeds_out, int32_t *n_chains, uint32_t *status,
@@ -506,23 +515,24 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t nsa = 0;
-    // this wave's 64 * cp.scratch bytes: each array lane-interleaved (SP); the workspace holds whole waves
-    const int lane = tid & 63;
-    uint8_t *wb = scratch + (size_t)(tid >> 6) * 64 * (size_t)cp.scratch;
-    ChainCtx C;
+    // S = 64: this wave's 64 * cp.scratch bytes, each array lane-interleaved (SP); the workspace holds whole
+    // waves.  S = 1 (retry workspaces): the thread's own cp.scratch bytes, arrays contiguous.
+    const int lane = S == 1 ? 0 : (tid & 63);
+    uint8_t *wb = scratch + (S == 1 ? (size_t)tid : (size_t)(tid >> 6) * 64) * (size_t)cp.scratch;
+    ChainCtx<S> C;
     C.cap_seeds = cp.seeds;
     C.cap_ch = cp.chains;
     C.cap_nodes = cp.chains / 2 + 8;
     size_t off = 0;
-    C.seeds = SP<SeedNode>{reinterpret_cast<SeedNode *>(wb) + lane};
-    off += (size_t)C.cap_seeds * 64 * sizeof(SeedNode);
-    C.ch = SP<ChainNode>{reinterpret_cast<ChainNode *>(wb + off) + lane};
-    off += (size_t)C.cap_ch * 64 * sizeof(ChainNode);
-    C.nodes = SP<KNode>{reinterpret_cast<KNode *>(wb + off) + lane};
-    off += (size_t)C.cap_nodes * 64 * sizeof(KNode);
-    SP<int> ord{reinterpret_cast<int *>(wb + off) + lane};
-    SP<int> kept_list = ord + cp.chains;
-    SP<int> stk = kept_list + cp.chains;   // introsort stack (192 ints), then the B-tree walk's (3 x 24)
+    C.seeds = SP<SeedNode, S>{reinterpret_cast<SeedNode *>(wb) + lane};
+    off += (size_t)C.cap_seeds * S * sizeof(SeedNode);
+    C.ch = SP<ChainNode, S>{reinterpret_cast<ChainNode *>(wb + off) + lane};
+    off += (size_t)C.cap_ch * S * sizeof(ChainNode);
+    C.nodes = SP<KNode, S>{reinterpret_cast<KNode *>(wb + off) + lane};
+    off += (size_t)C.cap_nodes * S * sizeof(KNode);
+    SP<int, S> ord{reinterpret_cast<int *>(wb + off) + lane};
+    SP<int, S> kept_list = ord + cp.chains;
+    SP<int, S> stk = kept_list + cp.chains;   // introsort stack (192 ints), then the B-tree walk's (3 x 24)
     for (int li = tid; li < n; li += nthr) {
         n_chains[li] = 0;
         if (status[li]) continue;
@@ -567,7 +577,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         // in-order traversal of the B-tree -> chain order
         int nord = 0;
         {   // iterative in-order walk == kbtree's __kb_traverse
-            SP<int> stn = stk + 192, sti = stn + 24, std_ = sti + 24;
+            SP<int, S> stn = stk + 192, sti = stn + 24, std_ = sti + 24;
             int sp = 0;
             stn[0] = C.root; sti[0] = 0; std_[0] = 0;
             if (!C.nodes[C.root].is_internal) {   // a lone leaf root (<= 9 chains, the common case): its keys
@@ -597,7 +607,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
             if (c.w >= o.min_chain_weight) ord[n_chn++] = ord[i];
         }
         if (n_chn > 0) {
-            const SP<ChainNode> ch = C.ch;
+            const SP<ChainNode, S> ch = C.ch;
             ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; }, stk);
             ch[ord[0]].kept = 3;
             int nk = 0;
@@ -1732,8 +1742,12 @@ hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts 
                         const int32_t *sel, int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains,
                         Seed *seeds, int32_t *n_chains, uint32_t *status, uint8_t *scratch, Counters *ctr)
 {
-    hipLaunchKernelGGL(k_chain, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds, n_chains,
-                       status, scratch, ctr);
+    if (sel)   // retry workspaces: a few reads per launch, contiguous per-thread scratch
+        hipLaunchKernelGGL(k_chain<1>, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds,
+                           n_chains, status, scratch, ctr);
+    else
+        hipLaunchKernelGGL(k_chain<64>, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds,
+                           n_chains, status, scratch, ctr);
     return hipGetLastError();
 }
 

@@ -252,6 +252,24 @@ extern "C" int64_t bsq_index_seq_len(const bsq_index *idx) { return idx ? (int64
 extern "C" int64_t bsq_index_primary(const bsq_index *idx) { return idx ? (int64_t)idx->h.primary : -1; }
 extern "C" int32_t bsq_index_n_refs(const bsq_index *idx) { return idx ? (int32_t)idx->h.anns.size() : -1; }
 
+extern "C" int bsq_index_same_refs(const bsq_index *a, const bsq_index *b)
+{
+    if (!a || !b) return -1;
+    const HostIndex &x = a->h, &y = b->h;
+    // (rows as added: l_pac is only set by a build, and a fresh index is compared against a built one)
+    if (x.anns.size() != y.anns.size() || x.holes.size() != y.holes.size() || x.pac.size() != y.pac.size())
+        return 0;
+    for (size_t i = 0; i < x.anns.size(); ++i) {
+        const Ann &p = x.anns[i], &q = y.anns[i];
+        if (p.offset != q.offset || p.len != q.len || p.n_ambs != q.n_ambs || p.id != q.id) return 0;
+    }
+    for (size_t i = 0; i < x.holes.size(); ++i) {
+        const Hole &p = x.holes[i], &q = y.holes[i];
+        if (p.offset != q.offset || p.len != q.len || p.amb != q.amb) return 0;
+    }
+    return x.pac.empty() || memcmp(x.pac.data(), y.pac.data(), x.pac.size()) == 0 ? 1 : 0;
+}
+
 static bool host_tables(const HostIndex &h) { return !h.occ.empty(); }   // false: device-built, not downloaded
 
 extern "C" int64_t bsq_index_sa(const bsq_index *idx, int64_t row)
@@ -772,8 +790,10 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
     // Every stage kernel derives its scratch pointer from the thread id but dereferences it only inside
     // `for (li = tid; li < n; ...)`; a retry workspace runs n <= max_reads reads per launch, so only
     // max_reads threads ever touch scratch (the main pass may run more reads than threads: full grid).
-    // (k_chain lays its state out per wave of 64 threads: whole waves)
-    w.scratch_total = (with_sel ? ((int64_t)std::max(max_reads, 1) + 63) / 64 * 64 : (int64_t)w.grid * 256) * w.cp.scratch;
+    // The main pass's k_chain lays its state out per wave of 64 threads (the grid is whole blocks); the retry
+    // kernels keep each thread's scratch contiguous (k_chain<1>), so a level-2 workspace of one read holds one
+    // read's scratch, not a wave's.
+    w.scratch_total = (with_sel ? (int64_t)std::max(max_reads, 1) : (int64_t)w.grid * 256) * w.cp.scratch;
     HIPCHK(hipMalloc(&w.scratch, (size_t)w.scratch_total));
     if (with_sel) HIPCHK(hipMalloc(&w.sel, R * 4));
     if (long_reads(cp.max_len)) HIPCHK(hipMalloc(&w.sscore, R * cp.seeds * 4));
@@ -1475,6 +1495,7 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         return BSQ_E_INVALID;
     }
     HIPCHK(hipSetDevice(b->device));
+    b->dev_whole = false;   // set again only when this run completes with the whole view in d_out
     const int n = b->n_reads;
     const DOpts o = make_dopts(*opts);
     hipStream_t st = b->stream;
@@ -1641,6 +1662,7 @@ extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
         return BSQ_E_INVALID;
     }
     HIPCHK(hipSetDevice(b->device));
+    b->dev_whole = false;   // the seeding run reuses d_out's workspace: the records there are stale
     const int n = b->n_reads;
     const DOpts o = make_dopts(*opts);
     b->seeded = false;

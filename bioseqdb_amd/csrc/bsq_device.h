@@ -31,11 +31,12 @@ inline int64_t intv_slot_at(int64_t li, int64_t k, int64_t cap) { return ((li >>
 inline int64_t intv_slot_reads(int64_t n) { return (n + 63) / 64 * 64; }
 
 #ifdef __HIP__
-// A lane's array interleaved with the other lanes of its wave: element i at p[i * 64].
-template <typename T> struct SP {
+// A lane's array interleaved with the other lanes of its wave: element i at p[i * S] (S = 64); S = 1 is the
+// contiguous per-thread layout (the retry kernels, which run a handful of reads per launch).
+template <typename T, int S = 64> struct SP {
     T *p;
-    __host__ __device__ T &operator[](int i) const { return p[(size_t)i * 64]; }
-    __host__ __device__ SP operator+(int i) const { return SP{p + (size_t)i * 64}; }
+    __host__ __device__ T &operator[](int i) const { return p[(size_t)i * S]; }
+    __host__ __device__ SP operator+(int i) const { return SP{p + (size_t)i * S}; }
 };
 __device__ inline int64_t intv_slot_at_d(int64_t li, int64_t k, int64_t cap) { return ((li >> 6) * cap + k) * 64 + (li & 63); }
 #endif

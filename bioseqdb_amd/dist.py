@@ -129,12 +129,14 @@ class RecordExchange:
         with ctx:
             recv = [r[:mx] for r in self.recv] if me_dst else None
             self.work = dist.gather(self.send[:mx], recv, dst=self.dst, group=self.group, async_op=True)
-            if me_dst and self.gpu:
-                self.work.wait()   # orders the side stream after the gather, without a host wait
-                for h, r, s in zip(self.host, self.recv, sizes):
-                    if s:
-                        h[:s].copy_(r[:s], non_blocking=True)
             if self.gpu:
+                # on every rank: the side stream (and the event recorded on it) follows the gather, so finish()
+                # waiting on the event means the send buffer may be refilled and the receive buffers read
+                self.work.wait()
+                if me_dst:
+                    for h, r, s in zip(self.host, self.recv, sizes):
+                        if s:
+                            h[:s].copy_(r[:s], non_blocking=True)
                 self.event = torch.cuda.Event()
                 self.event.record(self.stream)
         self.sizes = sizes

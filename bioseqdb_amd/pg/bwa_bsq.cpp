@@ -87,6 +87,8 @@ bool BwaIndex::empty() const { return bsq_index_l_pac(index_) <= 0; }
 
 int32_t BwaIndex::n_refs() const { return bsq_index_n_refs(index_); }
 
+bool BwaIndex::same_refs(const BwaIndex &o) const { return bsq_index_same_refs(index_, o.index_) == 1; }
+
 void BwaIndex::build()
 {
     if (empty()) return;   // bwa.cpp:108-109
@@ -314,6 +316,7 @@ void RefDigest::update(int64_t id, const void *nuclseq)
     h0 = mix(h0, t ^ (uint64_t)(n - i), 0x87C37B91114253D5ull);
     h1 ^= h0;
     ++rows;
+    bytes += n;
 }
 
 BwaIndexCache &BwaIndexCache::backend()
@@ -328,7 +331,7 @@ std::shared_ptr<BwaIndex> BwaIndexCache::get_or_build(const RefDigest &d, std::s
     const size_t cap = e ? (size_t)std::max(0, atoi(e)) : 2;
     std::lock_guard<std::mutex> lk(mu_);
     for (auto it = lru_.begin(); it != lru_.end(); ++it) {
-        if (it->d == d && it->devices == fresh->devices()) {
+        if (it->d == d && it->devices == fresh->devices() && it->idx->same_refs(*fresh)) {
             lru_.splice(lru_.begin(), lru_, it);
             ++hits_;
             return lru_.front().idx;

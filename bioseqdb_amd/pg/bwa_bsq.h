@@ -123,6 +123,7 @@ public:
 
     bool empty() const;          // no reference bases: align_* return no rows and draw no lrand48 value
     int32_t n_refs() const;
+    bool same_refs(const BwaIndex &o) const;   // given the same reference rows (the cache's content check)
     int device() const { return devices_[0]; }
     const std::vector<int> &devices() const { return devices_; }
 
@@ -153,10 +154,12 @@ private:
 uint64_t &bsq_backend_lrand48_calls();
 
 // Digest of a reference cursor: 128 bits over each row's id and nuclseq varlena bytes, in cursor order.
+// On a cache hit the index's own contents are compared too (BwaIndex::same_rows: row count, ids, lengths, bases
+// and holes), so a digest collision cannot hand back another reference's index.
 struct RefDigest {
-    uint64_t h0 = 0x9E3779B97F4A7C15ull, h1 = 0xC2B2AE3D27D4EB4Full, rows = 0;
+    uint64_t h0 = 0x9E3779B97F4A7C15ull, h1 = 0xC2B2AE3D27D4EB4Full, rows = 0, bytes = 0;
     void update(int64_t id, const void *nuclseq);
-    bool operator==(const RefDigest &o) const { return h0 == o.h0 && h1 == o.h1 && rows == o.rows; }
+    bool operator==(const RefDigest &o) const { return h0 == o.h0 && h1 == o.h1 && rows == o.rows && bytes == o.bytes; }
 };
 
 // Built indexes of this backend, most recently used first.  Capacity from

@@ -133,6 +133,9 @@ int64_t bsq_index_l_pac(const bsq_index *idx);
 int64_t bsq_index_seq_len(const bsq_index *idx);
 int64_t bsq_index_primary(const bsq_index *idx);
 int32_t bsq_index_n_refs(const bsq_index *idx);
+/* 1 when both indexes were given the same reference rows (ids, lengths, packed bases and holes, in order; built
+ * or not), else 0 (-1 for a NULL argument).  A backend's index cache confirms a digest hit with it. */
+int bsq_index_same_refs(const bsq_index *a, const bsq_index *b);
 /* Host copies of the logical FM quantities for tests (valid after build, no GPU needed):
  * sa[row] for row in [0, seq_len] and occ4 per row. */
 int64_t bsq_index_sa(const bsq_index *idx, int64_t row);

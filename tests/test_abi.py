@@ -50,3 +50,60 @@ def test_no_device_fails_loudly_without_fallback(gpu_available):
     with pytest.raises(BsqError) as e:
         idx.align_sequence(NucleotideSequence.from_text("ACGT" * 10))
     assert e.value.code == _native.BSQ_E_NODEV
+
+
+def test_index_same_refs_content_check():
+    """bsq_index_same_refs, the backend cache's confirmation of a digest hit: same rows -> 1; a changed base,
+    id, hole or row order -> 0 (host indexes, no GPU needed)."""
+    L = _native.lib()
+
+    def idx(rows):
+        h = ctypes.c_void_p()
+        _native.check(L.bsq_index_create(ctypes.byref(h)))
+        keep = []
+        for rid, t in rows:
+            ns = NucleotideSequence.from_text(t)
+            keep.append(ns)
+            _native.check(L.bsq_index_add_ref(h, rid, ns.ptr))
+        return h, keep
+
+    base = [(1, "ACGTTGCA" * 50 + "NNNN" + "GATTACA" * 30), (2, "CCGGTTAA" * 40)]
+    a, ka = idx(base)
+    variants = {
+        "same": (base, 1),
+        "base": ([(1, "ACGTTGCA" * 50 + "NNNN" + "GATTACA" * 29 + "GATTACC"), base[1]], 0),
+        "id": ([(3, base[0][1]), base[1]], 0),
+        "hole": ([(1, base[0][1].replace("NNNN", "NNNR")), base[1]], 0),
+        "order": ([base[1], base[0]], 0),
+    }
+    try:
+        for name, (rows, want) in variants.items():
+            b, kb = idx(rows)
+            try:
+                assert L.bsq_index_same_refs(a, b) == want, name
+            finally:
+                L.bsq_index_free(b)
+        assert L.bsq_index_same_refs(a, None) == -1
+    finally:
+        L.bsq_index_free(a)
+
+
+def test_library_is_up_to_date_with_its_sources():
+    """The prebuilt libbsq.so travels to the GPU box as it is: it must not be older than any source or header
+    it is built from (make -q: nothing to rebuild)."""
+    import shutil
+    import subprocess
+    if not shutil.which("make"):
+        pytest.skip("no make")
+    r = subprocess.run(["make", "-q", "-C", os.path.join(ROOT, "bioseqdb_amd", "csrc")], capture_output=True)
+    assert r.returncode == 0, "libbsq.so is stale: run make -C bioseqdb_amd/csrc"
+
+
+def test_index_same_refs_built_vs_fresh():
+    """A built (cached) index against a fresh one given the same rows: still the same rows."""
+    L = _native.lib()
+    a, b = BwaIndex(), BwaIndex()
+    for x in (a, b):
+        x.add_ref_sequence(7, NucleotideSequence.from_text("ACGTTGCANNGATTACA" * 40))
+    a.build()
+    assert L.bsq_index_same_refs(a.handle, b.handle) == 1
