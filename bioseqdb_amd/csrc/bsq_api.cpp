@@ -71,7 +71,7 @@ hipError_t launch_row_write(hipStream_t, const RenderView &, const int64_t *, ch
 hipError_t launch_sub_write(hipStream_t, const RenderView &, const int64_t *, char *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
-hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *);
+hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *, int);
 hipError_t launch_intv_counts(hipStream_t, int, const int32_t *, const uint32_t *, int64_t *);
 hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *, const uint32_t *, const int64_t *,
                             uint64_t *);
@@ -328,7 +328,7 @@ static void table_sizes(const HostIndex &h, uint64_t bytes[T_N], int &K, int &wi
     if (h.seq_len == 0) return;
     const uint64_t nblk = dev_only ? h.dev_nblk : h.occ.size();
     bytes[T_OCC] = nblk * sizeof(OccBlock);
-    bytes[T_OCC32] = wide ? 0 : nblk * 2 * sizeof(OccBlock32);
+    bytes[T_OCC32] = nblk * 2 * sizeof(OccBlock32) + (wide ? occ32_sup_count(2 * nblk) * sizeof(SupBlock) : 0);
     bytes[T_SA] = (h.seq_len + 1) * (wide ? 8 : 4);
     bytes[T_PAC] = h.pac.size() + 16;
     K = kmer_depth(h.seq_len);
@@ -351,7 +351,9 @@ static void set_view(DeviceIndex *d, const IndexMeta &m)
     v.seq_len = m.seq_len;
     v.l_pac = (int64_t)m.l_pac;
     v.wide = m.wide;
-    v.occ32 = m.wide ? nullptr : d->occ32;
+    v.occ32 = d->occ32;
+    v.sup = m.wide && d->occ32 ? reinterpret_cast<const SupBlock *>(d->occ32 + 2 * (m.table_bytes[T_OCC] / sizeof(OccBlock)))
+                               : nullptr;
     v.kmer = m.kmer_k ? d->kmer : nullptr;
     v.kmer_k = m.kmer_k;
 }
@@ -442,22 +444,9 @@ static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
                          hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(d->pac, h.pac.data(), h.pac.size(), hipMemcpyHostToDevice));
     }
-    if (h.seq_len > 0 && !m.wide) {
-        // 64-base blocks: half 0 of each 128-base block keeps its counts, half 1 adds the first 64 bases
-        std::vector<OccBlock32> o32(h.occ.size() * 2);
-        for (size_t b = 0; b < h.occ.size(); ++b) {
-            const OccBlock &B = h.occ[b];
-            const uint64_t hi = B.hi[0], lo = B.lo[0];
-            const uint32_t n3 = (uint32_t)__builtin_popcountll(hi & lo), n2 = (uint32_t)__builtin_popcountll(hi & ~lo);
-            const uint32_t n1 = (uint32_t)__builtin_popcountll(~hi & lo), n0 = 64u - n1 - n2 - n3;
-            OccBlock32 &a = o32[2 * b], &c = o32[2 * b + 1];
-            for (int t = 0; t < 4; ++t) a.cnt[t] = (uint32_t)B.cnt[t];
-            a.hi = B.hi[0]; a.lo = B.lo[0];
-            c.cnt[0] = (uint32_t)B.cnt[0] + n0; c.cnt[1] = (uint32_t)B.cnt[1] + n1;
-            c.cnt[2] = (uint32_t)B.cnt[2] + n2; c.cnt[3] = (uint32_t)B.cnt[3] + n3;
-            c.hi = B.hi[1]; c.lo = B.lo[1];
-        }
-        HIPCHK(hipMemcpy(d->occ32, o32.data(), o32.size() * sizeof(OccBlock32), hipMemcpyHostToDevice));
+    if (h.seq_len > 0) {   // 64-base blocks (+ superblocks for 64-bit rows) from the uploaded 128-base ones
+        HIPCHK(launch_occ32(nullptr, d->occ, (uint64_t)h.occ.size(), d->occ32, m.wide));
+        HIPCHK(hipDeviceSynchronize());
     }
     IndexMeta mv = m;
     mv.kmer_k = 0;
@@ -542,7 +531,7 @@ extern "C" int bsq_index_build_device(bsq_index *idx, int device)
     h.dev_rounds = rounds;
     h.dev_tied = tied;
     const IndexMeta m2 = meta_of(h);
-    if (!m2.wide && launch_occ32(nullptr, d->occ, nblk, d->occ32) != hipSuccess) { set_err("occ32 build"); return fail(BSQ_E_HIP); }
+    if (launch_occ32(nullptr, d->occ, nblk, d->occ32, m2.wide) != hipSuccess) { set_err("occ32 build"); return fail(BSQ_E_HIP); }
     IndexMeta mv = m2;
     mv.kmer_k = 0;
     set_view(d, mv);
@@ -1200,11 +1189,11 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         // u32 rows: 15 entries in LDS = 9.6 KB per one-wave block, 16 waves per CU; longer lists spill.
-        // 64-bit rows: the kernel's VGPRs allow 8 waves per CU, so 16 entries (18.4 KB) fit (C4 19.0 -> 21.8M
-        // reads/s against 8 entries).
+        // 64-bit rows: 150 VGPRs allow 12 waves per CU; 12 entries (13.8 KB per block, 11 waves) measured best
+        // (C4 seeding per 1M reads: 28.2 ms against 29.1 at 16 entries / 8 waves, 29.0 at 11, 30.4 at 10).
         // BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested (tests/test_gpu_parity.py).
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 16;
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 12;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
     } else {

@@ -24,6 +24,17 @@ struct alignas(32) OccBlock32 {
 };
 static_assert(sizeof(OccBlock32) == 32, "occ32 block must be 32 bytes");
 
+// 64-bit rows (texts of >= 2^32 rows, the 3 Gbp configs) use the same 32-B blocks with counts relative to
+// their superblock of 2^16 blocks (2^22 rows, so a relative count fits u32).  The superblocks' absolute counts
+// follow the blocks in the same table: cnt[c] = rows of base c before the superblock, gt[c] = rows of the bases
+// > c before it (the two sums bwt_extend needs per base).  1,431 superblocks (92 KB, cache-resident) at 3 Gbp.
+constexpr int SUP_SHIFT = 16;   // log2(64-base blocks per superblock)
+struct alignas(64) SupBlock {
+    uint64_t cnt[4], gt[4];
+};
+static_assert(sizeof(SupBlock) == 64, "superblock must be 64 bytes");
+inline uint64_t occ32_sup_count(uint64_t nblk32) { return (nblk32 >> SUP_SHIFT) + 1; }
+
 // Per-read interval slots (cap entries each) are laid out by wave of 64 reads: entry k of read li sits at
 // [((li / 64) * cap + k) * 64 + li % 64], so the lanes of a wave (one read each, in every kernel that
 // touches the slots) access the same entry index at adjacent addresses.  Workspaces hold whole waves.
@@ -58,7 +69,8 @@ struct DIndex {
     // interval (x[0], x[1], x[2], 0) that bwt_extend chains produce for S (u32 rows only), at entry
     // (4^|S| - 4)/3 + code(S), code = base-4 value of S with the first base most significant
     const uint32_t *kmer;
-    const OccBlock32 *occ32;  // 64-base rank blocks (u32 rows only; nullptr otherwise)
+    const OccBlock32 *occ32;  // 64-base rank blocks (absolute counts for u32 rows, superblock-relative otherwise)
+    const SupBlock *sup;      // 64-bit rows: superblock counts (after the blocks in the occ32 table); else nullptr
     int32_t wide;             // 1: 64-bit rows (seq_len >= 2^32, or forced by BSQ_FORCE_WIDE)
     int32_t pad2;
 };

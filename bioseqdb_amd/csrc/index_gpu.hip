@@ -613,12 +613,43 @@ __global__ void k_occ32(uint64_t nblk, const OccBlock *occ, OccBlock32 *o32)
         o32[2 * b + 1] = c;
     }
 }
+
+// 64-bit rows: the same blocks with counts relative to the superblock (2^16 64-base blocks = 2^15 OccBlocks),
+// and the superblocks' absolute counts after the 2 * nblk blocks (written by the thread of its first block)
+__global__ void k_occ32_wide(uint64_t nblk, const OccBlock *occ, OccBlock32 *o32, SupBlock *sup)
+{
+    GRID_LOOP(b, nblk) {
+        const OccBlock B = occ[b];
+        const uint64_t sb = (2 * b) >> SUP_SHIFT;
+        const OccBlock &S = occ[sb << (SUP_SHIFT - 1)];
+        const uint64_t hi = B.hi[0], lo = B.lo[0];
+        const uint32_t n3 = (uint32_t)__popcll(hi & lo), n2 = (uint32_t)__popcll(hi & ~lo), n1 = (uint32_t)__popcll(~hi & lo);
+        const uint32_t n0 = 64u - n1 - n2 - n3;
+        OccBlock32 a, c;
+        for (int t = 0; t < 4; ++t) a.cnt[t] = (uint32_t)(B.cnt[t] - S.cnt[t]);
+        a.hi = B.hi[0]; a.lo = B.lo[0];
+        c.cnt[0] = a.cnt[0] + n0; c.cnt[1] = a.cnt[1] + n1; c.cnt[2] = a.cnt[2] + n2; c.cnt[3] = a.cnt[3] + n3;
+        c.hi = B.hi[1]; c.lo = B.lo[1];
+        o32[2 * b] = a;
+        o32[2 * b + 1] = c;
+        if (((2 * b) & ((1ull << SUP_SHIFT) - 1)) == 0) {
+            SupBlock u;
+            for (int t = 0; t < 4; ++t) u.cnt[t] = S.cnt[t];
+            u.gt[3] = 0; u.gt[2] = S.cnt[3]; u.gt[1] = S.cnt[3] + S.cnt[2]; u.gt[0] = S.cnt[3] + S.cnt[2] + S.cnt[1];
+            sup[sb] = u;
+        }
+    }
+}
 }  // namespace
 
-hipError_t launch_occ32(hipStream_t st, const OccBlock *occ, uint64_t nblk, OccBlock32 *o32)
+hipError_t launch_occ32(hipStream_t st, const OccBlock *occ, uint64_t nblk, OccBlock32 *o32, int wide)
 {
     if (!nblk) return hipSuccess;
-    hipLaunchKernelGGL(k_occ32, grid_of(nblk), dim3(256), 0, st, nblk, occ, o32);
+    if (wide)
+        hipLaunchKernelGGL(k_occ32_wide, grid_of(nblk), dim3(256), 0, st, nblk, occ, o32,
+                           reinterpret_cast<SupBlock *>(o32 + 2 * nblk));
+    else
+        hipLaunchKernelGGL(k_occ32, grid_of(nblk), dim3(256), 0, st, nblk, occ, o32);
     return hipGetLastError();
 }
 

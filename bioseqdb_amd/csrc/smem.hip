@@ -24,7 +24,8 @@ namespace bsq {
 template <typename X>
 struct FM {
     const OccBlock *occ;
-    const OccBlock32 *occ32;   // 64-base blocks, used when X is u32
+    const OccBlock32 *occ32;   // 64-base blocks (superblock-relative counts when X is u64)
+    const SupBlock *sup;       // X = u64: superblock counts
     const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
     int K;
     // table entry idx: (x[0], x[2], x[1], 0) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B); (x[0], x[2])
@@ -124,6 +125,18 @@ DEV void occ_c32(const uint4 (&w)[2], uint32_t k, bool none, int c, uint32_t &cc
     cg = ((w[0].y & s0) + (w[0].z & (s0 | s1)) + (w[0].w & (s0 | s1 | s2)) + ng) & live;
 }
 
+// 64-bit rows: the same two sums from a superblock-relative 32-B block plus its superblock's counts (the
+// superblock table is small and cache-resident; its two words load beside the block).  Half the block bytes
+// and registers of the 128-base 64-B OccBlock, and one 64-bit plane word per popcount instead of two.
+DEV void occ_c32w(const uint4 (&w)[2], uint64_t k, bool none, int c, const SupBlock *sb, uint64_t &cc, uint64_t &cg)
+{
+    uint32_t rc, rg;
+    occ_c32(w, (uint32_t)k, false, c, rc, rg);
+    const uint64_t live = none ? 0ull : ~0ull;
+    cc = (sb->cnt[c] + rc) & live;
+    cg = (sb->gt[c] + rg) & live;
+}
+
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
 // used for the rank queries (x[1] forward, x[0] backward), `o` the other one.
 template <typename X>
@@ -143,14 +156,15 @@ DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, u
         occ_c32(wl, ll, false, c, lc, lg);
         nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
     } else {
-        const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ + (knone ? 0 : (kk >> 7)));
-        const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ + (ll >> 7));
-        uint4 wk[4], wl[4];
-        wk[0] = pk[0]; wk[1] = pk[1]; wk[2] = pk[2]; wk[3] = pk[3];
-        wl[0] = pl[0]; wl[1] = pl[1]; wl[2] = pl[2]; wl[3] = pl[3];
-        occ_c(wk, kk, knone, c, kc, kg);
-        occ_c(wl, ll, false, c, lc, lg);
-        nblk += (knone || (kk >> 7) == (ll >> 7)) ? 2 : 4;
+        const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ32 + (knone ? 0 : (kk >> 6)));
+        const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ32 + (ll >> 6));
+        const SupBlock *sk = fm.sup + (knone ? 0 : (kk >> (6 + SUP_SHIFT))), *sl = fm.sup + (ll >> (6 + SUP_SHIFT));
+        uint4 wk[2], wl[2];
+        wk[0] = pk[0]; wk[1] = pk[1];
+        wl[0] = pl[0]; wl[1] = pl[1];
+        occ_c32w(wk, kk, knone, c, sk, kc, kg);
+        occ_c32w(wl, ll, false, c, sl, lc, lg);
+        nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
     }
     na = fm.L2(c) + 1 + kc;
     nx2 = lc - kc;
@@ -188,29 +202,26 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
         if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
         if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
     } else {
-        const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ + (kan ? 0 : (kka >> 7)));
-        const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ + (lla >> 7));
-        const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ + (kbn ? 0 : (kkb >> 7)));
-        const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ + (llb >> 7));
-        uint4 w0[4], w1[4], w2[4], w3[4];
-        if (da) {
-            w0[0] = p0[0]; w0[1] = p0[1]; w0[2] = p0[2]; w0[3] = p0[3];
-            w1[0] = p1[0]; w1[1] = p1[1]; w1[2] = p1[2]; w1[3] = p1[3];
-        }
-        if (hb) {
-            w2[0] = p2[0]; w2[1] = p2[1]; w2[2] = p2[2]; w2[3] = p2[3];
-            w3[0] = p3[0]; w3[1] = p3[1]; w3[2] = p3[2]; w3[3] = p3[3];
-        }
-        occ_c(w0, kka, kan, c, kc, kg);
-        occ_c(w1, lla, false, c, lc, lg);
+        const uint4 *p0 = reinterpret_cast<const uint4 *>(fm.occ32 + (kan ? 0 : (kka >> 6)));
+        const uint4 *p1 = reinterpret_cast<const uint4 *>(fm.occ32 + (lla >> 6));
+        const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ32 + (kbn ? 0 : (kkb >> 6)));
+        const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ32 + (llb >> 6));
+        constexpr int SS = 6 + SUP_SHIFT;
+        const SupBlock *s0 = fm.sup + (kan ? 0 : (kka >> SS)), *s1 = fm.sup + (lla >> SS);
+        const SupBlock *s2 = fm.sup + (kbn ? 0 : (kkb >> SS)), *s3 = fm.sup + (llb >> SS);
+        uint4 w0[2], w1[2], w2[2], w3[2];
+        if (da) { w0[0] = p0[0]; w0[1] = p0[1]; w1[0] = p1[0]; w1[1] = p1[1]; }
+        if (hb) { w2[0] = p2[0]; w2[1] = p2[1]; w3[0] = p3[0]; w3[1] = p3[1]; }
+        occ_c32w(w0, kka, kan, c, s0, kc, kg);
+        occ_c32w(w1, lla, false, c, s1, lc, lg);
         ra0 = fm.L2(c) + 1 + kc;
         ra2 = lc - kc;
-        occ_c(w2, kkb, kbn, c, kc, kg);
-        occ_c(w3, llb, false, c, lc, lg);
+        occ_c32w(w2, kkb, kbn, c, s2, kc, kg);
+        occ_c32w(w3, llb, false, c, s3, lc, lg);
         rb0 = fm.L2(c) + 1 + kc;
         rb2 = lc - kc;
-        if (da) nblk += (kan || (kka >> 7) == (lla >> 7)) ? 2 : 4;
-        if (hb) nblk += (kbn || (kkb >> 7) == (llb >> 7)) ? 2 : 4;
+        if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
+        if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
     }
 }
 
@@ -269,22 +280,24 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
     int n = 0, i = x + 1;
     uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
     bool stop = false;               // the forward walk ended early (hole or interval below min_intv)
-    if constexpr (sizeof(X) == 4) {
+    {
         // Lengths 2..min(K, len - x) come from the k-mer table.  Their table rows depend only on the read's
         // bases, so every row is loaded before the first one is used (one round trip instead of K - 1);
         // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
+        // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
+        // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
         constexpr int KM = 11;   // kmer_depth() never exceeds 11
         const int Lt = fm.K < len - x ? fm.K : len - x;
         int cb[KM + 1];
 #pragma unroll
         for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
-        uint2 e[KM + 1];
+        X e0[KM + 1], e2[KM + 1];
         int nt = 1;   // bases from x covered without a hole (capped at Lt)
 #pragma unroll
         for (int t = 2; t <= KM; ++t) {
             if (nt == t - 1 && cb[t] < 4) {
                 fcode = fcode << 2 | (uint32_t)cb[t];
-                e[t] = reinterpret_cast<const uint2 *>(fm.kt)[2 * (size_t)(koff(t) + fcode)];
+                fm.kget02(koff(t) + fcode, e0[t], e2[t]);
                 nt = t;
             }
         }
@@ -294,7 +307,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
 #pragma unroll
             for (int t = 2; t <= KM; ++t) {
                 if (t <= nt && !stop) {
-                    const X n0 = e[t].x, n2 = e[t].y;
+                    const X n0 = e0[t], n2 = e2[t];
                     if (n2 != ik2) {
                         if (n >= L.total()) { ovf = true; return len; }
                         L.set(n++, ik0, ik2, ikend);
@@ -552,6 +565,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     FM<X> fm;
     fm.occ = ix.occ;
     fm.occ32 = ix.occ32;
+    fm.sup = ix.sup;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
@@ -699,6 +713,7 @@ __global__ void k_kmer_level(DIndex ix, void *tabv, int L)
     FM<X> fm;
     fm.occ = ix.occ;
     fm.occ32 = ix.occ32;
+    fm.sup = ix.sup;
     fm.kt = reinterpret_cast<const uint4 *>(tabv);
     fm.K = 0;
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2];
