@@ -328,7 +328,11 @@ DEV void ks_introsort(A a, int n, LT lt, S stk)
             int rp = a[k];
             if (k != t) { int x = a[k]; a[k] = a[t]; a[t] = x; }
             for (;;) {
-                do ++i; while (lt(a[i], rp));
+                // a[t] == rp is klib's sentinel (lt(rp, rp) is false), so `i < t` never changes where the scan
+                // stops; the explicit bound keeps the compiler from miscompiling this loop when `a` is a
+                // lane-interleaved index array (k_extend with S = 64 scratch hung deterministically on an unbounded
+                // scan and never with S = 1; with the bound both are exact)
+                do ++i; while (i < t && lt(a[i], rp));
                 do --j; while (i <= j && lt(rp, a[j]));
                 if (j <= i) break;
                 int x = a[i]; a[i] = a[j]; a[j] = x;
@@ -675,9 +679,10 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
 // (lane l's column j at lds[j * 64 + l]: every lane hits its own bank, so accesses never conflict).
 // ksw_extend2 keeps h and e in [0, h0 + qlen*max] (every candidate is clamped at 0), so u16 is exact
 // whenever the host-side bound check passes.
+template <class P>   // int2 * (contiguous) or SP<int2, S> (lane-interleaved)
 struct EhG {
     static constexpr bool kRing = false;
-    int2 *p;
+    P p;
     bool *ovf = nullptr;
     DEV int2 get(int j) const { return p[j]; }
     DEV void set(int j, int2 v) const { p[j] = v; }
@@ -903,8 +908,9 @@ DEVN int ksw_global2(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target
 // ksw_global2's score alone, inlined (mem_patch_reg's use in the extension stage): the same recurrences as
 // ksw_global2 above without the traceback, so the extension kernel makes no out-of-line call and needs no
 // private stack segment.
+template <class EHP>
 DEV int ksw_global2_score(const DOpts &o, int qlen, QAcc query, int tlen, TAcc target, int o_del, int e_del, int o_ins,
-                          int e_ins, int w, int2 *eh, uint64_t &cells)
+                          int e_ins, int w, EHP eh, uint64_t &cells)
 {
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
     const Score sc = score_of(o);
@@ -942,8 +948,9 @@ DEV int ksw_global2_score(const DOpts &o, int qlen, QAcc query, int tlen, TAcc t
 }
 
 // bwa_gen_cigar2's score for mem_patch_reg (no CIGAR)
+template <class EHP>
 DEV int gen_cigar2_score(const DIndex &ix, const DOpts &o, int w_, const uint8_t *q, int qb, int l_query, int64_t rb,
-                         int64_t re, int *score, int2 *eh, uint64_t &cells, uint64_t &bases)
+                         int64_t re, int *score, EHP eh, uint64_t &cells, uint64_t &bases)
 {
     if (l_query <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac)) return 0;
     const int64_t rlen = re - rb;
@@ -1193,13 +1200,18 @@ DEV uint64_t hash_64(uint64_t key)
     return key;
 }
 
+// The extension's lane-private scratch: S = 64 lays each array out interleaved across the 64 lanes of a wave
+// (element i of a lane at [i * 64 + lane] of the wave's region, SP), so a wave's same-index accesses share cache
+// lines; S = 1 keeps a thread's arrays contiguous (the retry pass, whose workspace holds one read's scratch per
+// thread).  Every array is typed SP<T, S>, so no code path can index it with the other layout.
+template <int S>
 struct ExtCtx {
-    Reg *av; int n, cap;
-    Reg *tmp;
-    int *idx;
-    uint64_t *srt;
-    int2 *eh;
-    int *stk;   // introsort stack (192 ints)
+    Reg *av; int n, cap;   // the read's regions: its own output slot (contiguous per read)
+    SP<Reg, S> tmp;
+    SP<int, S> idx;
+    SP<uint64_t, S> srt;
+    SP<int2, S> eh;
+    SP<int, S> stk;        // introsort stack (192 ints)
     bool ovf;
 };
 
@@ -1245,14 +1257,14 @@ DEV int ext_call(const DOpts &o, int qlen, QA query, int tlen, TAcc target, int 
                        gscore, max_off, ehx, cells);
 }
 
-template <class EH, class QM>
-DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
-                   const int32_t *sscore, ExtCtx &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
+// mem_chain2aln's reference window of a chain: [rmax0, rmax1) from every seed's maximal gaps, not crossing the
+// forward/reverse junction and clamped to the row (strand-flipped) that holds seeds[0] (bns_fetch_seq)
+DEV void chain_window(const DIndex &ix, const DOpts &o, int l_query, const Seed *seeds, int cn, int64_t &rmax0,
+                      int64_t &rmax1, uint64_t &bases)
 {
-    int64_t l_pac = ix.l_pac, rmax0, rmax1;
-    if (c.n == 0) return;
+    const int64_t l_pac = ix.l_pac;
     rmax0 = l_pac << 1; rmax1 = 0;
-    for (int i = 0; i < c.n; ++i) {
+    for (int i = 0; i < cn; ++i) {
         const Seed &t = seeds[i];
         int64_t b = t.rbeg - (t.qbeg + cal_max_gap(o, t.qbeg));
         int64_t e = t.rbeg + t.len + ((l_query - t.qbeg - t.len) + cal_max_gap(o, l_query - t.qbeg - t.len));
@@ -1265,52 +1277,86 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
         if (seeds[0].rbeg < l_pac) rmax1 = l_pac;
         else rmax0 = l_pac;
     }
-    {   // bns_fetch_seq: clamp to the row (strand-flipped) containing seeds[0]
-        int is_rev;
-        int rid = pos2rid(ix, depos(ix, seeds[0].rbeg, is_rev));
-        int64_t far_beg = ix.ann_off[rid], far_end = far_beg + ix.ann_len[rid];
-        if (is_rev) { int64_t t = far_beg; far_beg = (l_pac << 1) - far_end; far_end = (l_pac << 1) - t; }
-        rmax0 = rmax0 > far_beg ? rmax0 : far_beg;
-        rmax1 = rmax1 < far_end ? rmax1 : far_end;
-        bases += (uint64_t)((rmax1 - rmax0 + 3) >> 2);
-    }
-    uint64_t *srt = X.srt;
-    // seed score: len (mem_chain), or mem_flt_chained_seeds' score for long reads
-    for (int i = 0; i < c.n; ++i) srt[i] = (uint64_t)(uint32_t)(sscore ? sscore[i] : seeds[i].len) << 32 | (uint64_t)i;
-    for (int i = 1; i < c.n; ++i) {   // keys are unique: any correct sort equals ks_introsort_64
+    int is_rev;
+    int rid = pos2rid(ix, depos(ix, seeds[0].rbeg, is_rev));
+    int64_t far_beg = ix.ann_off[rid], far_end = far_beg + ix.ann_len[rid];
+    if (is_rev) { int64_t t = far_beg; far_beg = (l_pac << 1) - far_end; far_end = (l_pac << 1) - t; }
+    rmax0 = rmax0 > far_beg ? rmax0 : far_beg;
+    rmax1 = rmax1 < far_end ? rmax1 : far_end;
+    bases += (uint64_t)((rmax1 - rmax0 + 3) >> 2);
+}
+
+// the chain's seeds in ascending (score, index) order: mem_chain2aln visits srt[n-1] .. srt[0]; score = len
+// (mem_chain), or mem_flt_chained_seeds' score for long reads
+template <class SRT>
+DEV void seed_order(SRT srt, const Seed *seeds, const int32_t *sscore, int cn)
+{
+    for (int i = 0; i < cn; ++i) srt[i] = (uint64_t)(uint32_t)(sscore ? sscore[i] : seeds[i].len) << 32 | (uint64_t)i;
+    for (int i = 1; i < cn; ++i) {   // keys are unique: any correct sort equals ks_introsort_64
         uint64_t t = srt[i];
         int j = i;
         while (j > 0 && t < srt[j - 1]) { srt[j] = srt[j - 1]; --j; }
         srt[j] = t;
     }
+}
+
+// mem_chain2aln's test whether seed s (srt[k]) is skipped: contained in an existing region and not overlapping
+// a longer seed of the chain, visited earlier, on a different diagonal
+template <class SRT>
+DEV bool seed_skipped(const DOpts &o, int l_query, const Reg *av, int n_av, SRT srt, int k, int cn, const Seed *seeds,
+                      const Seed &s)
+{
+    int i;
+    for (i = 0; i < n_av; ++i) {
+        const Reg &p = av[i];
+        if (s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) continue;
+        if (s.len - p.seedlen0 > .1 * l_query) continue;
+        int qd = s.qbeg - p.qb;
+        int64_t rd = s.rbeg - p.rb;
+        int max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
+        int w = max_gap < p.w ? max_gap : p.w;
+        if (qd - rd < w && rd - qd < w) break;
+        qd = p.qe - (s.qbeg + s.len);
+        rd = p.re - (s.rbeg + s.len);
+        max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
+        w = max_gap < p.w ? max_gap : p.w;
+        if (qd - rd < w && rd - qd < w) break;
+    }
+    if (i == n_av) return false;
+    for (i = k + 1; i < cn; ++i) {
+        if (srt[i] == 0) continue;
+        const Seed &t = seeds[(uint32_t)srt[i]];
+        if (t.len < s.len * .95) continue;
+        if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && t.qbeg - s.qbeg != t.rbeg - s.rbeg) break;
+        if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && s.qbeg - t.qbeg != s.rbeg - t.rbeg) break;
+    }
+    return i == cn;
+}
+
+// the region's seed coverage and band once both extensions are done
+DEV void seed_finish(Reg &a, const Seed *seeds, int cn, int aw0, int aw1, int slen)
+{
+    a.seedcov = 0;
+    for (int i2 = 0; i2 < cn; ++i2) {
+        const Seed &t = seeds[i2];
+        if (t.qbeg >= a.qb && t.qbeg + t.len <= a.qe && t.rbeg >= a.rb && t.rbeg + t.len <= a.re) a.seedcov += t.len;
+    }
+    a.w = aw0 > aw1 ? aw0 : aw1;
+    a.seedlen0 = slen;
+}
+
+template <class EH, class QM, int S>
+DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t *q, const ChainDesc &c, const Seed *seeds,
+                   const int32_t *sscore, ExtCtx<S> &X, EH ehx, QM qm, uint64_t &cells, uint64_t &bases)
+{
+    int64_t rmax0, rmax1;
+    if (c.n == 0) return;
+    chain_window(ix, o, l_query, seeds, c.n, rmax0, rmax1, bases);
+    const SP<uint64_t, S> srt = X.srt;
+    seed_order(srt, seeds, sscore, c.n);
     for (int k = c.n - 1; k >= 0; --k) {
         const Seed s = seeds[(uint32_t)srt[k]];
-        int i;
-        for (i = 0; i < X.n; ++i) {
-            const Reg &p = X.av[i];
-            if (s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) continue;
-            if (s.len - p.seedlen0 > .1 * l_query) continue;
-            int qd = s.qbeg - p.qb;
-            int64_t rd = s.rbeg - p.rb;
-            int max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
-            int w = max_gap < p.w ? max_gap : p.w;
-            if (qd - rd < w && rd - qd < w) break;
-            qd = p.qe - (s.qbeg + s.len);
-            rd = p.re - (s.rbeg + s.len);
-            max_gap = cal_max_gap(o, qd < rd ? qd : (int)rd);
-            w = max_gap < p.w ? max_gap : p.w;
-            if (qd - rd < w && rd - qd < w) break;
-        }
-        if (i < X.n) {
-            for (i = k + 1; i < c.n; ++i) {
-                if (srt[i] == 0) continue;
-                const Seed &t = seeds[(uint32_t)srt[i]];
-                if (t.len < s.len * .95) continue;
-                if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && t.qbeg - s.qbeg != t.rbeg - s.rbeg) break;
-                if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && s.qbeg - t.qbeg != s.rbeg - t.rbeg) break;
-            }
-            if (i == c.n) { srt[k] = 0; continue; }
-        }
+        if (seed_skipped(o, l_query, X.av, X.n, srt, k, c.n, seeds, s)) { srt[k] = 0; continue; }
         if (X.n >= X.cap) { X.ovf = true; return; }
         Reg &a = X.av[X.n++];
         a = Reg{};
@@ -1360,17 +1406,12 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
                 a.truesc += gscore - sc0;
             }
         } else a.qe = l_query, a.re = s.rbeg + s.len;
-        a.seedcov = 0;
-        for (int i2 = 0; i2 < c.n; ++i2) {
-            const Seed &t = seeds[i2];
-            if (t.qbeg >= a.qb && t.qbeg + t.len <= a.qe && t.rbeg >= a.rb && t.rbeg + t.len <= a.re) a.seedcov += t.len;
-        }
-        a.w = aw0 > aw1 ? aw0 : aw1;
-        a.seedlen0 = s.len;
+        seed_finish(a, seeds, c.n, aw0, aw1, s.len);
     }
 }
 
-DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg &a, const Reg &b, int *_w, int2 *eh,
+template <class EHP>
+DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg &a, const Reg &b, int *_w, EHP eh,
                   uint64_t &cells, uint64_t &bases)
 {
     int w, score = 0, q_s, r_s;
@@ -1394,7 +1435,8 @@ DEV int patch_reg(const DIndex &ix, const DOpts &o, const uint8_t *q, const Reg 
     return score;
 }
 
-DEV void permute(ExtCtx &X, int n)
+template <int S>
+DEV void permute(ExtCtx<S> &X, int n)
 {
     bool ident = true;   // most region lists are already in order: skip the two copies through scratch
     for (int i = 0; i < n; ++i) ident = ident && X.idx[i] == i;
@@ -1403,7 +1445,8 @@ DEV void permute(ExtCtx &X, int n)
     for (int i = 0; i < n; ++i) X.av[i] = X.tmp[i];
 }
 
-DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, ExtCtx &X, uint64_t &cells, uint64_t &bases)
+template <int S>
+DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, ExtCtx<S> &X, uint64_t &cells, uint64_t &bases)
 {
     int n = X.n, m, i, j;
     if (n <= 1) return n;
@@ -1454,7 +1497,8 @@ DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, Ext
     return m;
 }
 
-DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
+template <int S>
+DEV void mark_primary_se(const DOpts &o, ExtCtx<S> &X, int64_t id)
 {
     int n = X.n;
     if (n == 0) return;
@@ -1470,7 +1514,8 @@ DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
     int tmp = o.a + o.b;
     tmp = o.o_del + o.e_del > tmp ? o.o_del + o.e_del : tmp;
     tmp = o.o_ins + o.e_ins > tmp ? o.o_ins + o.e_ins : tmp;
-    int *z = X.idx, nz = 0;
+    const SP<int, S> z = X.idx;
+    int nz = 0;
     z[nz++] = 0;
     for (int i = 1; i < n; ++i) {
         int k;
@@ -1492,7 +1537,7 @@ DEV void mark_primary_se(const DOpts &o, ExtCtx &X, int64_t id)
     }
 }
 
-template <bool LDS>
+template <bool LDS, int S>
 __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, Caps cp, const uint8_t *codes,
                                                            const int64_t *offs, const int32_t *sel, const int64_t *ids,
                                                            int n, const ChainDesc *chains, const Seed *seeds,
@@ -1503,13 +1548,20 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t cells = 0, bases = 0;
-    uint8_t *sb = scratch + (size_t)tid * cp.scratch;
-    ExtCtx X;
-    X.tmp = reinterpret_cast<Reg *>(sb);
-    X.idx = reinterpret_cast<int *>(sb + (size_t)cp.regs * sizeof(Reg));
-    X.srt = reinterpret_cast<uint64_t *>(sb + (size_t)cp.regs * sizeof(Reg) + (size_t)((cp.regs * 4 + 15) & ~15));
-    X.eh = reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(X.srt) + (size_t)cp.seeds * 8);
-    X.stk = reinterpret_cast<int *>(X.eh + cp.max_len + 2);
+    // S = 64: this wave's 64 * cp.scratch bytes, each array lane-interleaved; S = 1: the thread's own bytes
+    const int lane = S == 1 ? 0 : (tid & 63);
+    uint8_t *wb = scratch + (S == 1 ? (size_t)tid : (size_t)(tid >> 6) * 64) * (size_t)cp.scratch;
+    ExtCtx<S> X;
+    size_t off = 0;
+    X.tmp = SP<Reg, S>{reinterpret_cast<Reg *>(wb) + lane};
+    off += (size_t)cp.regs * S * sizeof(Reg);
+    X.idx = SP<int, S>{reinterpret_cast<int *>(wb + off) + lane};
+    off += (size_t)((cp.regs * 4 + 15) & ~15) * S;
+    X.srt = SP<uint64_t, S>{reinterpret_cast<uint64_t *>(wb + off) + lane};
+    off += (size_t)cp.seeds * S * 8;
+    X.eh = SP<int2, S>{reinterpret_cast<int2 *>(wb + off) + lane};
+    off += (size_t)(cp.max_len + 2) * S * sizeof(int2);
+    X.stk = SP<int, S>{reinterpret_cast<int *>(wb + off) + lane};
     for (int it = tid; it < n; it += nthr) {
         const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;
@@ -1531,7 +1583,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
             for (int c = 0; c < nc && !X.ovf; ++c)
                 chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
         } else {
-            EhG ehx{X.eh};
+            EhG<SP<int2, S>> ehx{X.eh};
             QMakeG qm{q};
             for (int c = 0; c < nc && !X.ovf; ++c)
                 chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
@@ -1811,13 +1863,16 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 && in4(o.mat_match) && in4(o.mat_mismatch) &&
                      in4(o.mat_amb) &&
                      (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
+    // Contiguous per-thread scratch (S = 1).  The lane-interleaved layout (S = 64, as k_chain's) measured slower
+    // here: lone 1M-read launch 7.0 ms against 6.67 ms, PMC fetch + write 1.17 GB against 1.28 GB -- the kernel is
+    // bound by VALU issue under divergence, not by its scratch traffic.
     if (lds) {
         const size_t sh = (size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2);
-        hipLaunchKernelGGL(k_extend<true>, dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n, chains,
-                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
+        hipLaunchKernelGGL((k_extend<true, 1>), dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n,
+                           chains, seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
     } else {
-        hipLaunchKernelGGL(k_extend<false>, dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains, seeds,
-                           n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
+        hipLaunchKernelGGL((k_extend<false, 1>), dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains,
+                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
     }
     return hipGetLastError();
 }

@@ -11,7 +11,7 @@ Usage: traffic_from_pmc.py <profile dir> <out json> <round tag>
 import csv, glob, json, os, sys
 
 # stage -> kernels its HIP events bracket (the sorts' rocprim kernels are negligible and not counted)
-KERNELS = {"smem": ["k_codes_wave", "k_smem_lds<unsigned int"], "chain": ["bsq::k_chain"],
+KERNELS = {"smem": ["k_codes_wave", "k_smem_lds<"], "chain": ["k_chain<"],
            "extend": ["k_ext_key", "k_extend<true>"],
            "reg2aln": ["k_r2a_key", "k_reg2aln_g<16>", "k_reg2aln_g<32>", "bsq::k_reg2aln_w"]}
 
@@ -36,10 +36,14 @@ def main(root, dst, tag):
     calib = {names[i]: round(c[2] / (gib if i != 3 else 96 * (1 << 20)), 4) for i, c in enumerate(cal[:6])}
     corr = calib.get("gather64_4G", 1.0)
     fetch, write = per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE"), per_dispatch(os.path.join(root, "write"), "WRITE_SIZE")
-    try:   # reads one launch of each stage processed in the profiled bench run (1M / --streams)
-        rpl = json.load(open(os.path.join(root, "fetch.json")))["config"]["reads_per_launch"]
+    # the profiled run: `--timed-only --streams 1 --steps 1 --warmup 0`, so every dispatch of a stage kernel belongs
+    # to the one lone launch over all the reads (C4: ten 1M-read workspace chunks, one dispatch each)
+    try:
+        bj = json.load(open(os.path.join(root, "fetch.json")))
+        rpl = bj["config"]["reads_per_launch"]
+        launches = bj["steps"] * bj["config"]["streams"]
     except (OSError, KeyError, ValueError):
-        rpl = 1000000
+        rpl, launches = 1000000, 1
     res = {"round": tag, "reads_per_launch": rpl, "fetch_correction": 1.0 / corr,
            "calibration_fetch_size_over_bytes": calib, "kernels": {}}
     for stage, pats in KERNELS.items():
@@ -50,8 +54,8 @@ def main(root, dst, tag):
             wk = [k for k in write if pat in k]
             if not fk or not wk:
                 continue
-            fb += sum(fetch[fk[0]]) / len(fetch[fk[0]])
-            wb += sum(write[wk[0]]) / len(write[wk[0]])
+            fb += sum(sum(fetch[k]) for k in fk) / launches
+            wb += sum(sum(write[k]) for k in wk) / launches
             names.append(fk[0].split("(")[0])
         if names:
             res["kernels"][stage] = {"kernel": " + ".join(names), "fetch_bytes": fb / corr, "write_bytes": wb,
