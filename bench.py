@@ -842,6 +842,7 @@ def main() -> int:
                     "conversion, alignment as concurrent shares, D2H, merged result arrays); first call includes "
                     "workspace allocation; repeat = median of 3"}
         L.bsq_hits_free(ho)
+        N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
 
         # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
         # (262144) reads submitted to a bsq_pipeline of depth 3 (each fetch staged, then its tuples released),

@@ -87,6 +87,7 @@ SIGNATURES = {
     "bsq_align_batch": (ctypes.c_int, [_P, ctypes.POINTER(Opts), ctypes.POINTER(_P), ctypes.c_int32,
                                        ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(Hits))]),
     "bsq_hits_free": (None, [ctypes.POINTER(Hits)]),
+    "bsq_index_release_pool": (ctypes.c_int, [_P]),
     "bsq_render_tsv": (_P, [_P, ctypes.POINTER(Hits), ctypes.POINTER(_P)]),
     "bsq_index_ref_subseq": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "bsq_free": (None, [_P]),

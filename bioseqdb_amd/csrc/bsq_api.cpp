@@ -57,6 +57,7 @@ hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, cons
                                 const int32_t *, const int32_t *);
 hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
+bool wide_z32(const DIndex &);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
@@ -1189,11 +1190,13 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         // u32 rows: 15 entries in LDS = 9.6 KB per one-wave block, 16 waves per CU; longer lists spill.
-        // 64-bit rows: 150 VGPRs allow 12 waves per CU; 12 entries (13.8 KB per block, 11 waves) measured best
-        // (C4 seeding per 1M reads: 28.2 ms against 29.1 at 16 entries / 8 waves, 29.0 at 11, 30.4 at 10).
-        // BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested (tests/test_gpu_parity.py).
+        // 64-bit rows: 148 VGPRs allow 12 waves per CU.  With u32 interval sizes (l_pac < 2^32: 14-B entries)
+        // 14 entries fill 12.5 KB per block at 12 waves (C4 seeding per 1M reads: 25.3 ms against 26.2 at 13,
+        // 27.3 at 12); all-u64 entries (18 B) measured best at 12 (28.2 ms against 29.1 at 16 entries / 8 waves,
+        // 29.0 at 11, 30.4 at 10).  BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested
+        // (tests/test_gpu_parity.py).
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : 12;
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : wide_z32(ix) ? 14 : 12;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
     } else {
@@ -2062,6 +2065,16 @@ extern "C" int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void 
     h->read_off[n_reads] = h->n_hits;
     release_all();
     *out = h;
+    return BSQ_OK;
+}
+
+extern "C" int bsq_index_release_pool(bsq_index *idx)
+{
+    if (!idx) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    std::unique_lock<std::mutex> lk(idx->pool_mu, std::try_to_lock);
+    if (!lk.owns_lock()) { set_err("the index's pooled pipeline is in use"); return BSQ_E_INVALID; }
+    bsq_pipeline_free(idx->pipe);
+    idx->pipe = nullptr;
     return BSQ_OK;
 }
 

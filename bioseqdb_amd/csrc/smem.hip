@@ -14,6 +14,7 @@
 // Restates algorithms of BWA (lh3/bwa, Apache-2.0) and klib (MIT) for bit-exact results; see NOTICE.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "bsq_device.h"
 
@@ -30,25 +31,27 @@ struct FM {
     int K;
     // table entry idx: (x[0], x[2], x[1], 0) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B); (x[0], x[2])
     // first, so the backward phase (which never reads x[1]) takes one 8-B (16-B) load per entry
-    DEV void kget(uint32_t idx, X &a0, X &a1, X &a2) const
+    template <typename Z>
+    DEV void kget(uint32_t idx, X &a0, X &a1, Z &a2) const
     {
         if constexpr (sizeof(X) == 4) {
             const uint4 e = kt[idx];
-            a0 = e.x; a2 = e.y; a1 = e.z;
+            a0 = e.x; a2 = (Z)e.y; a1 = e.z;
         } else {
             const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(kt) + 2 * (size_t)idx;
             const ulonglong2 u = p[0], v = p[1];
-            a0 = u.x; a2 = u.y; a1 = v.x;
+            a0 = u.x; a2 = (Z)u.y; a1 = v.x;
         }
     }
-    DEV void kget02(uint32_t idx, X &a0, X &a2) const
+    template <typename Z>
+    DEV void kget02(uint32_t idx, X &a0, Z &a2) const
     {
         if constexpr (sizeof(X) == 4) {
             const uint2 e = reinterpret_cast<const uint2 *>(kt)[2 * (size_t)idx];
-            a0 = e.x; a2 = e.y;
+            a0 = e.x; a2 = (Z)e.y;
         } else {
             const ulonglong2 u = reinterpret_cast<const ulonglong2 *>(kt)[2 * (size_t)idx];
-            a0 = u.x; a2 = u.y;
+            a0 = u.x; a2 = (Z)u.y;
         }
     }
     DEV X kget1(uint32_t idx) const
@@ -139,10 +142,12 @@ DEV void occ_c32w(const uint4 (&w)[2], uint64_t k, bool none, int c, const SupBl
 
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
 // used for the rank queries (x[1] forward, x[0] backward), `o` the other one.
-template <typename X>
-DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, uint64_t &nblk)
+// Z: the type of interval sizes x[2] -- u32 also for 64-bit rows when l_pac < 2^32 (an interval size is at most
+// the count of one base, <= l_pac), which takes a quarter of the u64 kernel's registers and list bytes off it.
+template <typename X, typename Z>
+DEV void extend1(const FM<X> &fm, X a, X o, Z x2, int c, X &na, X &no, Z &nx2, uint64_t &nblk)
 {
-    const X k = a - 1, l = a - 1 + x2;
+    const X k = a - 1, l = a - 1 + (X)x2;
     const bool knone = k == (X)-1;
     const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
     X kc, kg, lc, lg;
@@ -167,18 +172,18 @@ DEV void extend1(const FM<X> &fm, X a, X o, X x2, int c, X &na, X &no, X &nx2, u
         nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
     }
     na = fm.L2(c) + 1 + kc;
-    nx2 = lc - kc;
-    no = o + (X)(a <= fm.primary && a + x2 - 1 >= fm.primary) + (lg - kg);
+    nx2 = (Z)(lc - kc);
+    no = o + (X)(a <= fm.primary && a + (X)x2 - 1 >= fm.primary) + (lg - kg);
 }
 
 // Two independent backward extensions by the same base (entries of one bwt_smem1 backward level);
 // all four occ blocks are in flight together.  Backward extensions only need (x[0], x[2]).
-template <typename X>
-DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, int c, X &ra0, X &ra2, X &rb0, X &rb2,
+template <typename X, typename Z>
+DEV void ext_back2(const FM<X> &fm, X a0, Z a2, X b0, Z b2, bool da, bool hb, int c, X &ra0, Z &ra2, X &rb0, Z &rb2,
                    uint64_t &nblk)
 {
-    const X ka = a0 - 1, la = a0 - 1 + a2;
-    const X kb = hb ? b0 - 1 : ka, lb = hb ? b0 - 1 + b2 : la;
+    const X ka = a0 - 1, la = a0 - 1 + (X)a2;
+    const X kb = hb ? b0 - 1 : ka, lb = hb ? b0 - 1 + (X)b2 : la;
     const bool kan = ka == (X)-1, kbn = kb == (X)-1;
     const X kka = ka - (ka >= fm.primary), lla = la - (la >= fm.primary);
     const X kkb = kb - (kb >= fm.primary), llb = lb - (lb >= fm.primary);
@@ -194,11 +199,11 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
         occ_c32(w0, kka, kan, c, kc, kg);
         occ_c32(w1, lla, false, c, lc, lg);
         ra0 = fm.L2(c) + 1 + kc;
-        ra2 = lc - kc;
+        ra2 = (Z)(lc - kc);
         occ_c32(w2, kkb, kbn, c, kc, kg);
         occ_c32(w3, llb, false, c, lc, lg);
         rb0 = fm.L2(c) + 1 + kc;
-        rb2 = lc - kc;
+        rb2 = (Z)(lc - kc);
         if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
         if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
     } else {
@@ -215,11 +220,11 @@ DEV void ext_back2(const FM<X> &fm, X a0, X a2, X b0, X b2, bool da, bool hb, in
         occ_c32w(w0, kka, kan, c, s0, kc, kg);
         occ_c32w(w1, lla, false, c, s1, lc, lg);
         ra0 = fm.L2(c) + 1 + kc;
-        ra2 = lc - kc;
+        ra2 = (Z)(lc - kc);
         occ_c32w(w2, kkb, kbn, c, s2, kc, kg);
         occ_c32w(w3, llb, false, c, s3, lc, lg);
         rb0 = fm.L2(c) + 1 + kc;
-        rb2 = lc - kc;
+        rb2 = (Z)(lc - kc);
         if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
         if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
     }
@@ -242,22 +247,23 @@ template <> DEV uint32_t &lds_x<uint32_t>(int i) { return g_smem_u32[i]; }
 template <> DEV uint64_t &lds_x<uint64_t>(int i) { return g_smem_u64[i]; }
 template <typename T> DEV T spill_load(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 
-template <typename X>
+template <typename X, typename Z>
 struct LList {
-    int x0, x2, end;   // element offsets of this lane's entry 0: x0/x2 in X units, end in u16 units
+    int x0, x2, end;   // element offsets of this lane's entry 0: x0 in X units, x2 in Z units, end in u16 units
     int stride, cap;
-    X *gx0, *gx2;
+    X *gx0;
+    Z *gx2;
     uint32_t *gend;
     int gcap;
     DEV int total() const { return cap + gcap; }
-    DEV void set(int e, X a, X b, int en)
+    DEV void set(int e, X a, Z b, int en)
     {
-        if (e < cap) { lds_x<X>(x0 + e * stride) = a; lds_x<X>(x2 + e * stride) = b; g_smem_u16[end + e * stride] = (uint16_t)en; }
+        if (e < cap) { lds_x<X>(x0 + e * stride) = a; lds_x<Z>(x2 + e * stride) = b; g_smem_u16[end + e * stride] = (uint16_t)en; }
         else { const int g = e - cap; gx0[g] = a; gx2[g] = b; gend[g] = (uint32_t)en; }
     }
-    DEV void get(int e, X &a, X &b, int &en) const
+    DEV void get(int e, X &a, Z &b, int &en) const
     {
-        if (e < cap) { a = lds_x<X>(x0 + e * stride); b = lds_x<X>(x2 + e * stride); en = g_smem_u16[end + e * stride]; }
+        if (e < cap) { a = lds_x<X>(x0 + e * stride); b = lds_x<Z>(x2 + e * stride); en = g_smem_u16[end + e * stride]; }
         else { const int g = e - cap; a = spill_load(gx0 + g); b = spill_load(gx2 + g); en = (int)spill_load(gend + g); }
     }
 };
@@ -267,15 +273,16 @@ struct OutSlot {   // the read's output intervals (global, wave-interleaved), me
     int n, cap, n1;
 };
 
-template <typename X, typename Q>
-DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &L, OutSlot &S,
+template <typename X, typename Z, typename Q>
+DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S,
                   bool &ovf, uint64_t &nblk, uint64_t &nkm)
 {
     S.n1 = 0;
     if (q[x] > 3) return x + 1;
     if (min_intv < 1) min_intv = 1;
     int c0 = q[x];
-    X ik0 = fm.L2(c0) + 1, ik2 = fm.L2(c0 + 1) - fm.L2(c0), ik1 = fm.L2(3 - c0) + 1;
+    X ik0 = fm.L2(c0) + 1, ik1 = fm.L2(3 - c0) + 1;
+    Z ik2 = (Z)(fm.L2(c0 + 1) - fm.L2(c0));
     int ikend = x + 1;
     int n = 0, i = x + 1;
     uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
@@ -291,7 +298,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
         int cb[KM + 1];
 #pragma unroll
         for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
-        X e0[KM + 1], e2[KM + 1];
+        X e0[KM + 1];
+        Z e2[KM + 1];
         int nt = 1;   // bases from x covered without a hole (capped at Lt)
 #pragma unroll
         for (int t = 2; t <= KM; ++t) {
@@ -307,11 +315,12 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
 #pragma unroll
             for (int t = 2; t <= KM; ++t) {
                 if (t <= nt && !stop) {
-                    const X n0 = e0[t], n2 = e2[t];
+                    const X n0 = e0[t];
+                    const Z n2 = e2[t];
                     if (n2 != ik2) {
                         if (n >= L.total()) { ovf = true; return len; }
                         L.set(n++, ik0, ik2, ikend);
-                        if (n2 < (X)min_intv) { stop = true; i = x + t - 1; }
+                        if (n2 < (Z)min_intv) { stop = true; i = x + t - 1; }
                     }
                     if (!stop) { ik0 = n0; ik2 = n2; ikend = x + t; }
                 }
@@ -364,7 +373,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
         qi = i + 1 < len ? q[i + 1] : 0;   // prefetch the next base
         if (cur < 4) {
             const int c = 3 - cur;
-            X n1, n0, n2;
+            X n1, n0;
+            Z n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
                 fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
@@ -373,7 +383,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
             if (n2 != ik2) {
                 if (n >= L.total()) { ovf = true; return len; }
                 L.set(n++, ik0, ik2, ikend);
-                if (n2 < (X)min_intv) break;
+                if (n2 < (Z)min_intv) break;
             }
             ik0 = n0; ik1 = n1; ik2 = n2; ikend = i + 1;
         } else {
@@ -387,7 +397,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
         L.set(n++, ik0, ik2, ikend);
     }
     for (int j = 0; j < (n >> 1); ++j) {   // reverse: longest match first
-        X a0, a2, b0, b2;
+        X a0, b0;
+        Z a2, b2;
         int ae, be;
         L.get(j, a0, a2, ae);
         L.get(n - 1 - j, b0, b2, be);
@@ -395,7 +406,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
         L.set(n - 1 - j, a0, a2, ae);
     }
     int ret;
-    { X d0, d2; L.get(0, d0, d2, ret); }
+    { X d0; Z d2; L.get(0, d0, d2, ret); }
     int last_start = 0x7fffffff;
     const int K = fm.K;
     uint32_t wcode = 0;   // q[i .. i+K) packed, first base most significant (positions past the read: 0)
@@ -407,22 +418,25 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
     int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
     if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
     int nc = 0, j = 0;
-    X last_x2 = 0;
+    Z last_x2 = 0;
     for (;;) {
         {
             // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
             // Compaction writes go to nc <= j, below both entries already read.
             const bool hb = j + 1 < n;
-            X pa0, pa2, pb0, pb2;
+            X pa0, pb0;
+            Z pa2, pb2;
             int pae, pbe;
             L.get(j, pa0, pa2, pae);
             L.get(hb ? j + 1 : j, pb0, pb2, pbe);
-            X oa0 = 0, oa2 = 0, ob0 = 0, ob2 = 0;
+            X oa0 = 0, ob0 = 0;
+            Z oa2 = 0, ob2 = 0;
             if (c >= 0) {
                 // strings q[i .. end) of at most K bases come from the k-mer table
                 const int La = pae - i, Lb = pbe - i;
                 const bool ta = La <= K, tb = hb && Lb <= K;
-                X ea0 = 0, ea2 = 0, eb0 = 0, eb2 = 0;
+                X ea0 = 0, eb0 = 0;
+                Z ea2 = 0, eb2 = 0;
                 if (ta) fm.kget02(koff(La) + (wcode >> (2 * (K - La))), ea0, ea2);
                 if (tb) fm.kget02(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb2);
                 nkm += (uint64_t)ta + (uint64_t)tb;
@@ -432,9 +446,10 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
             }
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && !hb) break;
-                const X p0 = h ? pb0 : pa0, p2 = h ? pb2 : pa2, o0 = h ? ob0 : oa0, o2 = h ? ob2 : oa2;
+                const X p0 = h ? pb0 : pa0, o0 = h ? ob0 : oa0;
+                const Z p2 = h ? pb2 : pa2, o2 = h ? ob2 : oa2;
                 const int pe = h ? pbe : pae;
-                const bool keep_hit = c < 0 || o2 < (X)min_intv;
+                const bool keep_hit = c < 0 || o2 < (Z)min_intv;
                 if (keep_hit) {
                     if (nc == 0 && (S.n1 == 0 || i + 1 < last_start)) {
                         if (S.n + S.n1 >= S.cap) { ovf = true; return len; }
@@ -462,14 +477,15 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X> &
     return ret;
 }
 
-template <typename X, typename Q>
+template <typename X, typename Z, typename Q>
 DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int max_intv, Intv &mem,
                          uint64_t &nblk, uint64_t &nkm)
 {
     mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
     if (q[x] > 3) return x + 1;
     const int c0 = q[x];
-    X ik0 = fm.L2(c0) + 1, ik2 = fm.L2(c0 + 1) - fm.L2(c0), ik1 = fm.L2(3 - c0) + 1;
+    X ik0 = fm.L2(c0) + 1, ik1 = fm.L2(3 - c0) + 1;
+    Z ik2 = (Z)(fm.L2(c0 + 1) - fm.L2(c0));
     uint32_t fcode = (uint32_t)c0;
     int i0 = x + 1;
     if (fm.K > 1 && min_len >= fm.K) {
@@ -495,13 +511,14 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int 
         qi = i + 1 < len ? q[i + 1] : 0;
         if (cur < 4) {
             const int c = 3 - cur;
-            X n1, n0, n2;
+            X n1, n0;
+            Z n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
                 fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
-            if (n2 < (X)max_intv && i - x >= min_len) {
+            if (n2 < (Z)max_intv && i - x >= min_len) {
                 mem.x[0] = n0; mem.x[1] = n1; mem.x[2] = n2;
                 mem.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
                 return i + 1;
@@ -543,23 +560,23 @@ __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const 
     for (int i = (int)(threadIdx.x >> 6); i < len; i += 4) d[(size_t)i * 64] = g_codes_stage[s + i];
 }
 
-template <typename X, typename Q>
+template <typename X, typename Z, typename Q>
 __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
 {
     const int T = blockDim.x, t = threadIdx.x;
-    LList<X> L;
+    LList<X, Z> L;   // LDS: [x0: T*lcap X][x2: T*lcap Z][end: T*lcap u16]
     L.x0 = t;
-    L.x2 = T * lcap + t;
-    L.end = (int)((size_t)2 * T * lcap * sizeof(X) / 2) + t;
+    L.x2 = (int)((size_t)T * lcap * sizeof(X) / sizeof(Z)) + t;
+    L.end = (int)((size_t)T * lcap * (sizeof(X) + sizeof(Z)) / 2) + t;
     L.stride = T;
     L.cap = lcap;
-    {   // spill area: [x0: n*gcap X][x2: n*gcap X][end: n*gcap u32], this read's gcap entries of each
+    {   // spill area: [x0: n*gcap X][x2: n*gcap Z][end: n*gcap u32], this read's gcap entries of each
         const size_t me = (size_t)(blockIdx.x * T + t) * (size_t)gcap, tot = (size_t)n * (size_t)gcap;
         L.gx0 = reinterpret_cast<X *>(spill) + me;
-        L.gx2 = reinterpret_cast<X *>(spill) + tot + me;
-        L.gend = reinterpret_cast<uint32_t *>(spill + 2 * tot * sizeof(X)) + me;
+        L.gx2 = reinterpret_cast<Z *>(spill + tot * sizeof(X)) + me;
+        L.gend = reinterpret_cast<uint32_t *>(spill + tot * (sizeof(X) + sizeof(Z))) + me;
         L.gcap = spill ? gcap : 0;
     }
     FM<X> fm;
@@ -612,7 +629,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             while (x < len && !ovf) {
                 if (q[x] < 4) {
                     Intv m;
-                    x = seed_strategy1_x(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm);
+                    x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm);
                     if (m.x[2] > 0) {
                         if (S.n >= S.cap) { ovf = true; break; }
                         Intv &d = S.a[S.n++];
@@ -645,8 +662,16 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
 }
 
 // LDS bytes per thread for `lcap` list entries
-template <typename X>
-static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (2 * sizeof(X) + 2); }
+template <typename X, typename Z>
+static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (sizeof(X) + sizeof(Z) + 2); }
+
+// 64-bit rows whose interval sizes fit u32 (every x[2] is at most one base's count, <= l_pac); BSQ_FORCE_WIDE=2
+// (tests) takes the all-u64 kernel on any index
+bool wide_z32(const DIndex &ix)
+{
+    const char *fw = getenv("BSQ_FORCE_WIDE");
+    return !(fw && *fw == '2') && ix.l_pac < ((int64_t)1 << 32);
+}
 
 // codes_t: a workspace buffer of ceil(n / 64) * 64 * cp.max_len bytes for the wave-transposed copy of the
 // reads (nullptr: the kernel reads the packed codes)
@@ -663,21 +688,29 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
     if (!ix.wide) {
-        size_t sh = lds_bytes<uint32_t>(T, lcap);
+        size_t sh = lds_bytes<uint32_t, uint32_t>(T, lcap);
         if (codes_t)
-            hipLaunchKernelGGL((k_smem_lds<uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, intv,
-                               n_intv, status, ctr, lcap, spill, gcap, L);
+            hipLaunchKernelGGL((k_smem_lds<uint32_t, uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
+                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
         else
-            hipLaunchKernelGGL((k_smem_lds<uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs,
-                               n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
+            hipLaunchKernelGGL((k_smem_lds<uint32_t, uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
+    } else if (wide_z32(ix)) {   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
+        size_t sh = lds_bytes<uint64_t, uint32_t>(T, lcap);
+        if (codes_t)
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
+                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
+        else
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
     } else {
-        size_t sh = lds_bytes<uint64_t>(T, lcap);
+        size_t sh = lds_bytes<uint64_t, uint64_t>(T, lcap);
         if (codes_t)
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, intv,
-                               n_intv, status, ctr, lcap, spill, gcap, L);
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint64_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
+                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
         else
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes, offs,
-                               n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
+            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint64_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
     }
     return hipGetLastError();
 }

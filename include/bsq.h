@@ -228,6 +228,9 @@ int64_t bsq_lrand48_at(uint64_t pos);
 int bsq_align_batch(bsq_index *idx, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
                     uint64_t first_call_seq, bsq_hits **out);
 void bsq_hits_free(bsq_hits *hits);
+/* Frees the batches and workspaces bsq_align_batch keeps with the index between calls (a backend done with a
+ * large cursor gives the device memory back; the next call re-creates them).  BSQ_E_INVALID while in use. */
+int bsq_index_release_pool(bsq_index *idx);
 
 /* Renders hits as bwa_result rows (TSV, one line per hit, columns as bioseqdb--0.0.0.sql:196-212
  * without query_id): ref_id ref_subseq ref_match_start ref_match_end ref_match_len query_subseq

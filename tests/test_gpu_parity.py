@@ -121,11 +121,17 @@ def test_parity_smem_list_spill(monkeypatch):
     assert not bad, bad[:20]
 
 
-def test_parity_wide_rows(monkeypatch):
+@pytest.mark.parametrize("force,lcap", [("1", None), ("2", None), ("1", "2"), ("2", "2")],
+                         ids=["z32", "z64", "z32_spill", "z64_spill"])
+def test_parity_wide_rows(monkeypatch, force, lcap):
     """The 64-bit-row code path of the 3 Gbp configs (u64 SA, u64 SMEM lists with global spill, the u64
-    seeding kernel), forced on a small reference.  The k-mer table is built here too (K = 10 at this
-    size, kmer_depth in bsq_api.cpp); the real 3 Gbp index is tested in test_gpu_c4.py."""
-    monkeypatch.setenv("BSQ_FORCE_WIDE", "1")
+    seeding kernel), forced on a small reference.  BSQ_FORCE_WIDE=1 takes the kernel with u32 interval
+    sizes (what 3 Gbp references < 2^32 bases run), =2 the all-u64 one; lcap 2 sends nearly every SMEM
+    list into the global spill area.  The k-mer table is built here too (K = 10 at this size,
+    kmer_depth in bsq_api.cpp); the real 3 Gbp index is tested in test_gpu_c4.py."""
+    monkeypatch.setenv("BSQ_FORCE_WIDE", force)
+    if lcap:
+        monkeypatch.setenv("BSQ_TEST_LCAP", lcap)
     ref = synth.make_reference(1_000_000, n_rows=3, n_run_every=300_000, n_run_len=400)
     reads = synth.make_reads(ref, 3000, seed=31)
     pi, oi = build_pair([t.decode() for t in ref.texts()])

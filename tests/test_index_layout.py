@@ -45,4 +45,8 @@ def test_layout_wide(monkeypatch):
     mb = ctypes.c_uint64()
     assert L.bsq_index_layout(pi.handle, sizes, None, ctypes.byref(mb)) == 0
     n = L.bsq_index_seq_len(pi.handle)
-    assert sizes[1] == 0 and sizes[2] == (n + 1) * 8 and sizes[7] % 32 == 0
+    nblk = (n + 127) // 128 + 1
+    # 64-bit rows also get the 32-B blocks (u32 counts relative to 2^22-row superblocks), the superblocks'
+    # 64-B absolute counts appended (bsq_device.h SupBlock, one per 2^16 blocks of 64 rows)
+    assert sizes[1] == 2 * nblk * 32 + ((2 * nblk >> 16) + 1) * 64
+    assert sizes[2] == (n + 1) * 8 and sizes[7] % 32 == 0
