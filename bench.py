@@ -112,6 +112,9 @@ def default_opts(n_refs: int) -> N.Opts:
 
 
 CONFIGS = {
+    "c1": dict(reads=10_000, ref_bp=1_000_000, rows=1, seeding=False, metric=METRIC,
+               label="C1: 10k 150 bp reads vs 1 Mbp synthetic reference, full seed + extension + CIGAR (BASELINE.json "
+                     "configs[0]: the reference's own CPU-runnable case; latency-bound at this size)"),
     "c3": dict(reads=1_000_000, ref_bp=100_000_000, rows=1, seeding=False, metric=METRIC,
                label="C3: 150 bp reads vs 100 Mbp synthetic reference, full seed + banded SW extension + CIGAR "
                      "(BASELINE.json configs[2]); bwa_opts() SQL defaults"),

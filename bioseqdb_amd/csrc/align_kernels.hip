@@ -1376,6 +1376,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
                                       o.zdrop, s.len * o.a, &qle, &tle, &gtle, &gscore, &max_off0, ehx, cells);
                 if (a.score == prev || max_off0 < (aw0 >> 1) + (aw0 >> 2)) break;
             }
+            if (X.ovf) return;   // ring overflow: the retry pass redoes this read
             if (gscore <= 0 || gscore <= a.score - o.pen_clip5) {
                 a.qb = s.qbeg - qle, a.rb = s.rbeg - tle;
                 a.truesc = a.score;
@@ -1398,6 +1399,7 @@ DEV void chain2aln(const DIndex &ix, const DOpts &o, int l_query, const uint8_t 
                                       ehx, cells);
                 if (a.score == prev || max_off1 < (aw1 >> 1) + (aw1 >> 2)) break;
             }
+            if (X.ovf) return;
             if (gscore <= 0 || gscore <= a.score - o.pen_clip3) {
                 a.qe = qe + qle, a.re = rmax0 + re + tle;
                 a.truesc += a.score - sc0;

@@ -95,7 +95,9 @@ DEV int mat_sc(const DOpts &o, int t, int q)
 // (int)((double)x / d + k) -- libbwa's band and gap-length formulas -- in integers (d > 0, |x| < 2^31): the
 // double quotient is within an ulp of x/d, which lies at least 1/d from the next integer unless it is one, and
 // both the conversion and C's integer division truncate toward zero, so the two agree for every input
-DEV int idiv_plus(int x, int d, int k) { return (x + k * d) / d; }
+// d is a gap-extension penalty (a kernel argument, uniform across the wave): the SQL default 1 takes a scalar
+// branch around the ~30-instruction integer division
+DEV int idiv_plus(int x, int d, int k) { return d == 1 ? x + k : (x + k * d) / d; }
 
 DEV int infer_bw(int l1, int l2, int score, int a, int q, int r)
 {
