@@ -515,6 +515,8 @@ def main() -> int:
     ap.add_argument("--group-devices", default=None,
                     help="in-process group (--gpus N without torchrun): comma-separated device of each member "
                          "(default 0..N-1; a repeated device makes replicas on one GPU, for tests)")
+    ap.add_argument("--cursor-depth", type=int, default=8,
+                    help="fetches in flight in the sql_cursor measurement (BwaIndex::pipeline_depth's default)")
     ap.add_argument("--seed-offset", type=int, default=0,
                     help="rank (or member) k aligns the reads of seed READ_SEED + k + offset, lrand48 position "
                          "(k + offset) * reads: lets a one-GPU run reproduce any member of a multi-GPU run")
@@ -848,11 +850,11 @@ def main() -> int:
         N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
 
         # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
-        # (262144) reads submitted to a bsq_pipeline of depth 3 (each fetch staged, then its tuples released),
+        # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (8) (each fetch staged, then its tuples released),
         # the oldest fetch's rows taken when the pipeline is full; with the two nuclseq columns per row
         # (build_tuple_bwa) rendered on the GPU, and without them
         hb.phase = "pipelined cursor fetches"
-        fetch, depth, passes = 262144, 4, 4   # a 4M-read cursor: the batch's reads 4 times (16 fetches)
+        fetch, depth, passes = 262144, args.cursor_depth, 4   # a 4M-read cursor: the batch's reads 4 times (16 fetches)
 
         t_sub, sub_s = [0.0], [0.0]
 

@@ -54,7 +54,7 @@ hipError_t launch_collect_overflow(hipStream_t, int, const uint32_t *, int32_t *
 hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *,
                                 const int64_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *,
                                 uint32_t *, Counters *, int, uint8_t *, int64_t, int, int32_t *, int32_t *, int32_t *,
-                                const int32_t *, const int32_t *);
+                                const int32_t *, const int32_t *, int32_t *);
 hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
 bool wide_z32(const DIndex &);
@@ -160,6 +160,8 @@ extern "C" int bsq_device_count(void)
     return n;
 }
 
+// BSQ_R2A_DIAG=0: no lane-per-read diagonal pass before the reg2aln group kernels (A/B measurements)
+static bool no_r2a_diag() { const char *e = getenv("BSQ_R2A_DIAG"); return e && *e == '0'; }
 static bool tiny_caps() { const char *e = getenv("BSQ_TEST_TINY_CAPS"); return e && *e && *e != '0'; }
 
 static int default_threads()
@@ -314,7 +316,7 @@ static int kmer_depth(uint64_t seq_len)
     if (seq_len == 0) return 0;
     int K = 0;
     while (K < 11 && (1ull << (2 * (K + 1))) <= seq_len) ++K;   // ~log4(rows), at most 11
-    if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(13, atoi(e)));
+    if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(11, atoi(e)));   // the kernels' preload cap
     return K;
 }
 
@@ -827,6 +829,7 @@ struct bsq_batch {
     bsq_index *idx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t cstream = nullptr;  // the nuclseq columns (high priority: created on first use)
     int32_t max_reads = 0;
     int64_t max_bases = 0;
     int32_t n_reads = 0;
@@ -993,6 +996,7 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->ns_dev); hipFree(b->ns_meta);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
     if (b->stream) hipStreamDestroy(b->stream);
+    if (b->cstream && b->cstream != b->stream) { hipStreamSynchronize(b->cstream); hipStreamDestroy(b->cstream); }
     delete b;
 }
 
@@ -1250,7 +1254,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         }
         HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
                                     w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
-                                    w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr));
+                                    w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr,
+                                    r_order && !no_r2a_diag() ? w.eidx0 : nullptr));
     } else {
         HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.regs, w.n_regs, w.hits, w.cigars,
                               w.n_cig, w.status, w.scratch, b->ctr));
@@ -1792,10 +1797,9 @@ static int index_render_holes(bsq_index *idx, const RenderHole **d, int64_t *n)
 // Device inputs of the GPU renderers: the last run's records (still in HBM when the run was one chunk without
 // retried reads, else uploaded from the host view), the reference holes, the reads' own holes.  Every buffer is
 // the batch's or the index's (grow-only): nothing is allocated or freed in a steady loop.
-static int render_inputs(bsq_batch *b, const void *const *reads, RenderView &v)
+static int render_inputs(bsq_batch *b, const void *const *reads, RenderView &v, hipStream_t st)
 {
     const bsq_hits &H = b->view;
-    hipStream_t st = b->stream;
     const HostIndex &h = b->idx->h;
     const bsq_hit *dh = b->d_out;
     const uint32_t *dc = b->d_out_cig;
@@ -1851,7 +1855,7 @@ extern "C" int bsq_batch_render(bsq_batch *b, const void *const *reads, const ch
     HIPCHK(hipSetDevice(b->device));
     hipStream_t st = b->stream;
     RenderView v{};
-    { const int rc = render_inputs(b, reads, v); if (rc) return rc; }
+    { const int rc = render_inputs(b, reads, v, st); if (rc) return rc; }
     HIPCHK(launch_row_len(st, v, b->r_len));
     HIPCHK(hipMemsetAsync(b->r_len + H.n_hits, 0, 8, st));
     size_t tb = 0;
@@ -2272,7 +2276,20 @@ int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **ou
     const bsq_hits &H = b->view;
     const int64_t n = 2 * H.n_hits;
     HIPCHK(hipSetDevice(b->device));
-    hipStream_t st = b->stream;
+    // The columns run after the batch's alignment, while the pipeline's other slots align: on a stream of the
+    // device's greatest priority their small kernels are dispatched ahead of the queued alignment workgroups,
+    // so the oldest fetch's rows (the ones the backend waits for) are not held behind the younger fetches'
+    // seeding (BSQ_COLS_PRIORITY=0: the batch's own stream)
+    if (!b->cstream) {
+        const char *e = getenv("BSQ_COLS_PRIORITY");
+        if (e && *e == '0') b->cstream = b->stream;
+        else {
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&b->cstream, hipStreamNonBlocking, hi));
+        }
+    }
+    hipStream_t st = b->cstream;
     std::vector<int64_t> toff((size_t)n + 1, 0), poff((size_t)n + 1, 0);
     for (int64_t k = 0; k < H.n_hits; ++k) {
         const bsq_hit &x = H.hits[k];
@@ -2290,7 +2307,7 @@ int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **ou
     HIPCHK(b->arena.get(d_toff, (size_t)n + 1));
     if (H.n_hits) {
         RenderView v{};
-        { const int rc = render_inputs(b, reads, v); if (rc) return rc; }
+        { const int rc = render_inputs(b, reads, v, st); if (rc) return rc; }
         HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
         HIPCHK(launch_sub_write(st, v, d_toff, d_text));
     }

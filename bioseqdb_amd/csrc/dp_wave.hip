@@ -837,15 +837,167 @@ hipError_t launch_r2a_key(hipStream_t st, const DOpts &o, const Caps &cp, const 
     return hipGetLastError();
 }
 
+// ================================================================================================
+// Diagonal pass: one lane per read.  Most regions of 150-bp reads are gapless with a few mismatches, and
+// bwa_gen_cigar2 returns "nM" for them without a DP (w == 0, diagonal_wins, or the exact detour test).  This
+// kernel decides that per region sequentially in one lane (no LDS, every lane busy) and writes the read's
+// records when every region of it is decided; a read with any region that needs the DP is appended (in
+// input order, wave-aggregated) to `defer`, and the group kernel recomputes the whole read from scratch, so
+// the output does not depend on which kernel produced it.  The per-region control is k_reg2aln_g's.
+// ================================================================================================
+
+// gen_cigar2_g's diagonal shortcut for one region, sequential: the diagonal score S of the n x n problem and
+// whether w == 0, diagonal_wins(S) or detour_free(S) holds (detour_free's prefix sums / minima carried in a
+// single pass: C1/Cm the sums of delta before j, m1/mm their running minima including C[0] = 0).
+// Sequential reader of the query bases codes[a], codes[a + step], ... (step +-1) within [lo, hi]: 16-B aligned
+// words of the batch's code buffer, the next one loaded while the current one is consumed (a byte load per base
+// would wait on memory every step of the loop).
+struct QStream {
+    const uint8_t *codes;
+    int64_t a, wlo, whi, cur_w;
+    int step;
+    uint4 cur, nxt;
+    DEV uint4 load(int64_t w) const
+    {
+        return (w >= wlo && w <= whi) ? *reinterpret_cast<const uint4 *>(codes + 16 * w) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    DEV void init(const uint8_t *c, int64_t start, int dir, int64_t lo, int64_t hi)
+    {
+        codes = c; a = start; step = dir; wlo = lo >> 4; whi = hi >> 4;
+        cur_w = a >> 4;
+        cur = load(cur_w);
+        nxt = load(cur_w + step);
+    }
+    DEV int next()
+    {
+        const int64_t w = a >> 4;
+        if (w != cur_w) { cur = w == cur_w + step ? nxt : load(w); cur_w = w; nxt = load(w + step); }
+        const int k = (int)(a & 15);
+        const uint32_t v = (k & 8) ? ((k & 4) ? cur.w : cur.z) : ((k & 4) ? cur.y : cur.x);
+        a += step;
+        return (int)((v >> ((k & 3) << 3)) & 0xffu);
+    }
+};
+
+DEV bool diag_decides(const DIndex &ix, const DOpts &o, const Score sc, int w_, const uint8_t *codes, int64_t rd,
+                      int l_read, int q_start, int q_dir, int64_t t_start, int t_dir, int n, int &S)
+{
+    TStream ts;
+    ts.init(ix, t_start, t_dir);
+    QStream qs;
+    qs.init(codes, rd + q_start, q_dir, rd, rd + l_read - 1);
+    int tj = ts.next(), qj = qs.next();
+    int sum = 0, c1 = 0, cm = 0, m1 = 0, mm = 0, x = -0x3fffffff;
+    for (int j = 0; j < n; ++j) {
+        const bool nx = j + 1 < n;
+        const int tn = nx ? ts.next() : 0, qn = nx ? qs.next() : 0;
+        const int s0 = sc(tj, qj);
+        sum += s0;
+        m1 = m1 < c1 ? m1 : c1;
+        mm = mm < cm ? mm : cm;
+        const int a1 = c1 - m1 - s0, am = cm - mm - s0;
+        x = x > a1 ? x : a1;
+        x = x > am ? x : am;
+        if (nx) { c1 += sc(tj, qn) - s0; cm += sc(tn, qj) - s0; }
+        tj = tn; qj = qn;
+    }
+    S = sum;
+    if (w_ == 0 || diagonal_wins(o, n, sum)) return true;
+    const int64_t bound2 = (int64_t)(n - 2) * o.mat_max - (o.o_ins + o.o_del + 2 * (o.e_ins + o.e_del));
+    return (int64_t)sum > bound2 && (int64_t)x < (int64_t)(o.o_ins + o.e_ins + o.o_del + o.e_del);
+}
+
+__global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps cp, const uint8_t *__restrict__ codes,
+                                                      const int64_t *__restrict__ offs, int n,
+                                                      const int32_t *__restrict__ list, const int32_t *__restrict__ list_n,
+                                                      const Reg *__restrict__ regs, const int32_t *__restrict__ n_regs,
+                                                      Hit *__restrict__ hits, uint32_t *__restrict__ cigars,
+                                                      int32_t *__restrict__ n_cig_read, const uint32_t *__restrict__ status,
+                                                      int32_t *__restrict__ defer, int32_t *__restrict__ defer_n,
+                                                      Counters *ctr)
+{
+    const int n_items = list ? *list_n : n;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int li = k < n_items ? (list ? list[k] : k) : -1;
+    bool dfr = false;
+    uint64_t bases = 0;
+    if (li >= 0) {
+        if (status[li]) n_cig_read[li] = 0;
+        else {
+            const int64_t rd = offs[li];
+            const int l_read = (int)(offs[li + 1] - rd);
+            const int nr = n_regs[li];
+            const Score sc = score_of(o);
+            int tot = 0;
+            dfr = cp.cigar < 3;   // "nM" plus two clips; smaller CIGAR slots take the group kernel's overflow path
+            for (int g = 0; g < nr && !dfr; ++g) {
+                const Reg &ar = regs[(size_t)li * cp.regs + g];
+                const int qb = ar.qb, qe = ar.qe, lq = qe - qb;
+                const int64_t rb = ar.rb, re = ar.re, rlen = re - rb;
+                // gen_cigar2_g's early exits and the DP case belong to the group kernel
+                if (lq <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac) || re > (ix.l_pac << 1) || rb < 0 ||
+                    rlen != lq) { dfr = true; break; }
+                int tmp = infer_bw(lq, (int)rlen, ar.truesc, o.a, o.o_del, o.e_del);
+                int w2 = infer_bw(lq, (int)rlen, ar.truesc, o.a, o.o_ins, o.e_ins);
+                w2 = w2 > tmp ? w2 : tmp;
+                if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
+                w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+                const bool rev = rb >= ix.l_pac;
+                int S = 0;
+                if (!diag_decides(ix, o, sc, w2, codes, rd, l_read, rev ? qb + lq - 1 : qb, rev ? -1 : 1,
+                                  rev ? re - 1 : rb, rev ? -1 : 1, lq, S)) { dfr = true; break; }
+                // the retry loop of k_reg2aln_g: a second call (doubled band) when the first band was not the
+                // widest and S < truesc - a; it decides the same way (the shortcut does not depend on w > 0)
+                bases += (uint64_t)((rlen + 3) >> 2);
+                if (w2 != o.w << 2 && S < ar.truesc - o.a) bases += (uint64_t)((rlen + 3) >> 2);
+                uint32_t *cig = cigars + ((size_t)li * cp.regs + g) * cp.cigar;
+                int is_rev;
+                (void)depos(ix, rb < ix.l_pac ? rb : re - 1, is_rev);
+                int ncig = 0;
+                const int clip5 = is_rev ? l_read - qe : qb, clip3 = is_rev ? qb : l_read - qe;
+                if (clip5) cig[ncig++] = (uint32_t)clip5 << 4 | 3;
+                cig[ncig++] = (uint32_t)lq << 4;
+                if (clip3) cig[ncig++] = (uint32_t)clip3 << 4 | 3;
+                Hit hh;
+                hh.rb = rb; hh.re = re; hh.qb = qb; hh.qe = qe; hh.rid = ar.rid; hh.score = ar.score;
+                hh.flag = ar.secondary >= 0 ? 0x100 : 0;
+                hh.is_rev = is_rev; hh.n_cigar = ncig; hh.pad = 0;
+                hits[(size_t)li * cp.regs + g] = hh;
+                tot += ncig;
+            }
+            if (!dfr) n_cig_read[li] = tot;
+        }
+    }
+    // deferred reads keep their input order: one atomic per wave, lanes placed by the ballot's prefix
+    const uint64_t m = __ballot(dfr);
+    int base = 0;
+    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(defer_n, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (dfr) defer[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = li;
+    wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
+}
+
 // group kernels G = 16 then 32 over the reads (in `order` when given), the whole-wave kernel over what remains
+// dn: 4 counters -- [0], [1] the group kernels' defer lists, [3] the diagonal pass's ([2] is order_n's home);
+// pre: n entries for the diagonal pass's list (nullptr: no diagonal pass)
 hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                                 const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
                                 uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
                                 uint8_t *zslab, int64_t zslab_bytes, int max_blocks, int32_t *d0, int32_t *d1,
-                                int32_t *dn, const int32_t *order, const int32_t *order_n)
+                                int32_t *dn, const int32_t *order, const int32_t *order_n, int32_t *pre)
 {
     hipError_t e = hipMemsetAsync(dn, 0, 2 * sizeof(int32_t), st);
     if (e != hipSuccess) return e;
+    if (pre && n > 0) {
+        e = hipMemsetAsync(dn + 3, 0, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_reg2aln_diag, dim3((n + 255) / 256), dim3(256), 0, st, ix, o, cp, codes, offs, n, order,
+                           order_n, regs, n_regs, hits, cigars, n_cig, status, pre, dn + 3, ctr);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        order = pre;
+        order_n = dn + 3;
+    }
     e = launch_g<16>(st, ix, o, cp, codes, offs, n, order, order_n, regs, n_regs, hits, cigars, n_cig, status, d0,
                      dn, ctr, zcap, max_blocks);
     if (e != hipSuccess) return e;

@@ -15,6 +15,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -57,7 +60,20 @@ struct Slot {
     const uint8_t *col_buf = nullptr;     // the batch's pinned column buffers (borrowed)
     const int64_t *col_off = nullptr;
     std::thread th;
+    uint64_t job = 0;                     // submission number (alignment turns go in this order)
+    double t[6] = {0, 0, 0, 0, 0, 0};     // BSQ_PIPE_TRACE: submit, start, uploaded, run, columns, taken (ms)
 };
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool pipe_trace()
+{
+    static const bool on = [] { const char *e = getenv("BSQ_PIPE_TRACE"); return e && *e && *e != '0'; }();
+    return on;
+}
 
 }  // namespace
 
@@ -65,6 +81,9 @@ struct bsq_pipeline {
     bsq_index *idx = nullptr;
     std::vector<std::unique_ptr<Slot>> s;
     uint64_t n_submit = 0, n_take = 0, n_release = 0;   // slot of job j is s[j % S]
+    uint64_t run_started = 0;                           // jobs whose alignment turn has begun
+    int running = 0, run_cap = 4;                       // alignments on the device now, and at most
+    std::vector<std::array<double, 7>> trace;           // BSQ_PIPE_TRACE: per job, slot then Slot::t
     std::mutex mu;
     std::condition_variable cv;
     bool stop = false;
@@ -78,9 +97,10 @@ void drop_cols(Slot &x)
     x.col_off = nullptr;
 }
 
-// The job of one slot, on its worker thread.
-int run_job(bsq_pipeline *p, Slot &x)
+// Fetch staging (a deferred job) and the upload of its reads: before the slot's turn on the device.
+int prep_job(bsq_pipeline *p, Slot &x)
 {
+    x.t[1] = now_ms();
     if (x.mode == PipeMode::DEFER) {
         x.resident = false;
         const int rc = stage_nuclseqs(x.stage, x.reads, x.n);
@@ -88,14 +108,7 @@ int run_job(bsq_pipeline *p, Slot &x)
     } else if (x.mode == PipeMode::COPY) {
         x.resident = false;
     }
-    if (x.n == 0 || bsq_index_seq_len(p->idx) <= 0) {   // bwa.cpp:142-143: no region for any read
-        x.zeros.assign((size_t)x.n + 1, 0);
-        x.empty = bsq_hits{};
-        x.empty.n_reads = x.n;
-        x.empty.read_off = x.zeros.data();
-        x.view = &x.empty;
-        return BSQ_OK;
-    }
+    if (x.n == 0 || bsq_index_seq_len(p->idx) <= 0) return BSQ_OK;
     if (!x.batch || x.cap_reads < x.stage.n || x.cap_bases < x.stage.bases) {
         bsq_batch_free(x.batch);
         x.batch = nullptr;
@@ -113,15 +126,38 @@ int run_job(bsq_pipeline *p, Slot &x)
         if (rc) return rc;
         x.resident = true;
     }
+    return BSQ_OK;
+}
+
+// The alignment itself, in the slot's turn (at most run_cap jobs align at once, started in submission order).
+int align_job(bsq_pipeline *p, Slot &x)
+{
+    x.t[2] = now_ms();
+    if (x.n == 0 || bsq_index_seq_len(p->idx) <= 0) {   // bwa.cpp:142-143: no region for any read
+        x.zeros.assign((size_t)x.n + 1, 0);
+        x.empty = bsq_hits{};
+        x.empty.n_reads = x.n;
+        x.empty.read_off = x.zeros.data();
+        x.view = &x.empty;
+        return BSQ_OK;
+    }
     { const int rc = bsq_batch_run(x.batch, &x.opts, x.first_call); if (rc) return rc; }
+    x.t[3] = now_ms();
     x.view = bsq_batch_hits(x.batch);
-    if (x.cols && x.view->n_hits > 0) {
+    return BSQ_OK;
+}
+
+// build_tuple_bwa's two nuclseq columns, after the slot's turn (the next job aligns meanwhile)
+int cols_job(Slot &x)
+{
+    if (x.cols && x.view != &x.empty && x.view->n_hits > 0) {
         // the staged varlenas carry the reads' hole symbols (the caller's may be gone)
         std::vector<const void *> ptrs((size_t)x.n);
         for (int32_t i = 0; i < x.n; ++i) ptrs[(size_t)i] = x.stage.host + x.stage.meta[(size_t)i];
         const int rc = batch_render_cols(x.batch, ptrs.data(), &x.col_buf, &x.col_off);
         if (rc) return rc;
     }
+    x.t[4] = now_ms();
     return BSQ_OK;
 }
 
@@ -132,7 +168,22 @@ void worker(bsq_pipeline *p, Slot *x)
         p->cv.wait(lk, [&] { return p->stop || x->state == SlotState::QUEUED; });
         if (p->stop) return;
         lk.unlock();
-        const int rc = run_job(p, *x);
+        int rc = prep_job(p, *x);
+        // Alignment turns go in submission order, at most run_cap at once: a deeper pipeline keeps fetches staged
+        // and uploaded ahead, so a new alignment starts the moment one ends instead of the pipeline refilling
+        // in lockstep groups when the caller takes the oldest fetch (every job takes its turn, failed or not).
+        lk.lock();
+        p->cv.wait(lk, [&] { return x->job == p->run_started && p->running < p->run_cap; });
+        ++p->run_started;
+        ++p->running;
+        p->cv.notify_all();
+        lk.unlock();
+        if (!rc) rc = align_job(p, *x);
+        lk.lock();
+        --p->running;
+        p->cv.notify_all();
+        lk.unlock();
+        if (!rc) rc = cols_job(*x);
         const std::string err = rc ? std::string(bsq_last_error()) : std::string();
         lk.lock();
         x->rc = rc;
@@ -167,6 +218,7 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
     }
     if (mode == PipeMode::RERUN && x->stage.n != n_reads)
         return fail(BSQ_E_INVALID, "re-run of a different read count than the slot's staged reads");
+    const double t_submit = now_ms();
     if (mode == PipeMode::COPY) {   // staged on the caller's thread: the caller may release its reads on return
         x->resident = false;
         const int rc = stage_nuclseqs(x->stage, reads, n_reads);
@@ -181,6 +233,9 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
     x->reads = mode == PipeMode::DEFER ? reads : nullptr;
     x->view = nullptr;
     drop_cols(*x);
+    for (double &t : x->t) t = 0;
+    x->t[0] = t_submit;
+    x->job = p->n_submit;
     x->state = SlotState::QUEUED;
     ++p->n_submit;
     p->cv.notify_all();
@@ -192,6 +247,7 @@ int pipeline_rewind(bsq_pipeline *p)
     std::lock_guard<std::mutex> lk(p->mu);
     if (p->n_release != p->n_submit) return fail(BSQ_E_INVALID, "pipeline has outstanding submissions");
     p->n_submit = p->n_take = p->n_release = 0;
+    p->run_started = 0;
     return BSQ_OK;
 }
 
@@ -203,6 +259,13 @@ int pipeline_next_ex(bsq_pipeline *p, const bsq_hits **view, const uint8_t **col
     if (p->n_take == p->n_submit) return fail(BSQ_E_INVALID, "no submission to take");
     Slot *x = p->s[p->n_take % p->s.size()].get();
     p->cv.wait(lk, [&] { return x->state == SlotState::DONE; });
+    if (pipe_trace()) {
+        x->t[5] = now_ms();
+        std::array<double, 7> r{};
+        r[0] = (double)(p->n_take % p->s.size());
+        for (int k = 0; k < 6; ++k) r[(size_t)k + 1] = x->t[k];
+        p->trace.push_back(r);
+    }
     ++p->n_take;
     if (x->rc) {   // consumed: the slot is free again (its submission produced no rows)
         const int rc = x->rc;
@@ -229,6 +292,11 @@ extern "C" int bsq_pipeline_create(bsq_index *idx, int n_slots, bsq_pipeline **o
     std::unique_ptr<bsq_pipeline> p(new (std::nothrow) bsq_pipeline());
     if (!p) return fail(BSQ_E_NOMEM, "out of memory");
     p->idx = idx;
+    {   // concurrent alignments: 4 measure best on one MI355X (3-6 within 1 %, 8 lose 20 %)
+        const char *e = getenv("BSQ_PIPE_RUN");
+        const int v = e ? atoi(e) : 4;
+        p->run_cap = std::max(1, std::min(v > 0 ? v : 4, 64));
+    }
     for (int k = 0; k < n_slots; ++k) p->s.emplace_back(new Slot());
     for (auto &x : p->s) x->th = std::thread(worker, p.get(), x.get());
     *out = p.release();
@@ -248,6 +316,12 @@ extern "C" void bsq_pipeline_free(bsq_pipeline *p)
         });
         p->stop = true;
         p->cv.notify_all();
+    }
+    if (pipe_trace() && !p->trace.empty()) {   // one line per job, ms relative to the first submission
+        const double t0 = p->trace[0][1];
+        for (const auto &r : p->trace)
+            fprintf(stderr, "bsq_pipe slot %d submit %.2f start %.2f turn %.2f run %.2f cols %.2f taken %.2f\n",
+                    (int)r[0], r[1] - t0, r[2] - t0, r[3] - t0, r[4] - t0, r[5] - t0, r[6] - t0);
     }
     for (auto &x : p->s) {
         if (x->th.joinable()) x->th.join();

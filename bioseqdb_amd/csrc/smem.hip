@@ -161,15 +161,38 @@ DEV void extend1(const FM<X> &fm, X a, X o, Z x2, int c, X &na, X &no, Z &nx2, u
         occ_c32(wl, ll, false, c, lc, lg);
         nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
     } else {
+        // The two ends of an interval almost always share a superblock (2^22 rows): then the interval's size and
+        // the rank difference of the bases > c are differences of the blocks' relative u32 counts, and only the
+        // k end's cnt[c] (for the new x0) is read from the superblock table.
         const uint4 *pk = reinterpret_cast<const uint4 *>(fm.occ32 + (knone ? 0 : (kk >> 6)));
         const uint4 *pl = reinterpret_cast<const uint4 *>(fm.occ32 + (ll >> 6));
-        const SupBlock *sk = fm.sup + (knone ? 0 : (kk >> (6 + SUP_SHIFT))), *sl = fm.sup + (ll >> (6 + SUP_SHIFT));
+        constexpr int SS = 6 + SUP_SHIFT;
+        const X sbk = knone ? 0 : (kk >> SS), sbl = ll >> SS;
         uint4 wk[2], wl[2];
         wk[0] = pk[0]; wk[1] = pk[1];
         wl[0] = pl[0]; wl[1] = pl[1];
-        occ_c32w(wk, kk, knone, c, sk, kc, kg);
-        occ_c32w(wl, ll, false, c, sl, lc, lg);
+        const X base_k = fm.sup[sbk].cnt[c];
+        uint32_t rck, rgk, rcl, rgl;
+        occ_c32(wk, (uint32_t)kk, knone, c, rck, rgk);
+        occ_c32(wl, (uint32_t)ll, false, c, rcl, rgl);
         nblk += (knone || (kk >> 6) == (ll >> 6)) ? 1 : 2;
+        const X kc0 = knone ? (X)0 : base_k + rck;
+        X dgt;
+        Z dx2;
+        if (!knone && sbk == sbl) {
+            dx2 = (Z)(rcl - rck);
+            dgt = (X)(rgl - rgk);
+        } else {
+            const SupBlock *sl = fm.sup + sbl;
+            const X lc1 = sl->cnt[c] + rcl, lg1 = sl->gt[c] + rgl;
+            const X kg1 = knone ? (X)0 : fm.sup[sbk].gt[c] + rgk;
+            dx2 = (Z)(lc1 - kc0);
+            dgt = lg1 - kg1;
+        }
+        na = fm.L2(c) + 1 + kc0;
+        nx2 = dx2;
+        no = o + (X)(a <= fm.primary && a + (X)x2 - 1 >= fm.primary) + dgt;
+        return;
     }
     na = fm.L2(c) + 1 + kc;
     nx2 = (Z)(lc - kc);
@@ -212,19 +235,24 @@ DEV void ext_back2(const FM<X> &fm, X a0, Z a2, X b0, Z b2, bool da, bool hb, in
         const uint4 *p2 = reinterpret_cast<const uint4 *>(fm.occ32 + (kbn ? 0 : (kkb >> 6)));
         const uint4 *p3 = reinterpret_cast<const uint4 *>(fm.occ32 + (llb >> 6));
         constexpr int SS = 6 + SUP_SHIFT;
-        const SupBlock *s0 = fm.sup + (kan ? 0 : (kka >> SS)), *s1 = fm.sup + (lla >> SS);
-        const SupBlock *s2 = fm.sup + (kbn ? 0 : (kkb >> SS)), *s3 = fm.sup + (llb >> SS);
+        // as in extend1: the size is a difference of relative counts when both ends share a superblock, and only
+        // the k end's cnt[c] is read from the superblock table (backward extensions never need the gt sums)
+        const X sa0 = kan ? 0 : (kka >> SS), sa1 = lla >> SS, sb0 = kbn ? 0 : (kkb >> SS), sb1 = llb >> SS;
         uint4 w0[2], w1[2], w2[2], w3[2];
         if (da) { w0[0] = p0[0]; w0[1] = p0[1]; w1[0] = p1[0]; w1[1] = p1[1]; }
         if (hb) { w2[0] = p2[0]; w2[1] = p2[1]; w3[0] = p3[0]; w3[1] = p3[1]; }
-        occ_c32w(w0, kka, kan, c, s0, kc, kg);
-        occ_c32w(w1, lla, false, c, s1, lc, lg);
-        ra0 = fm.L2(c) + 1 + kc;
-        ra2 = (Z)(lc - kc);
-        occ_c32w(w2, kkb, kbn, c, s2, kc, kg);
-        occ_c32w(w3, llb, false, c, s3, lc, lg);
-        rb0 = fm.L2(c) + 1 + kc;
-        rb2 = (Z)(lc - kc);
+        const X base_a = fm.sup[sa0].cnt[c], base_b = fm.sup[sb0].cnt[c];
+        uint32_t rk, rg_, rl;
+        occ_c32(w0, (uint32_t)kka, kan, c, rk, rg_);
+        occ_c32(w1, (uint32_t)lla, false, c, rl, rg_);
+        const X ka0 = kan ? (X)0 : base_a + rk;
+        ra0 = fm.L2(c) + 1 + ka0;
+        ra2 = (!kan && sa0 == sa1) ? (Z)(rl - rk) : (Z)(fm.sup[sa1].cnt[c] + rl - ka0);
+        occ_c32(w2, (uint32_t)kkb, kbn, c, rk, rg_);
+        occ_c32(w3, (uint32_t)llb, false, c, rl, rg_);
+        const X kb0 = kbn ? (X)0 : base_b + rk;
+        rb0 = fm.L2(c) + 1 + kb0;
+        rb2 = (!kbn && sb0 == sb1) ? (Z)(rl - rk) : (Z)(fm.sup[sb1].cnt[c] + rl - kb0);
         if (da) nblk += (kan || (kka >> 6) == (lla >> 6)) ? 1 : 2;
         if (hb) nblk += (kbn || (kkb >> 6) == (llb >> 6)) ? 1 : 2;
     }
