@@ -42,7 +42,7 @@ METRIC = "aligned reads/sec (150 bp vs 100 Mbp ref) at 1/2/4/8 MI355X; bit-exact
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # stage -> the main-pass kernel its HIP events bracket (libbsq run_stages)
 STAGE_KERNEL = {"smem": "k_codes_wave+k_smem_lds", "chain": "k_chain", "extend": "k_ext_key+sort+k_extend",
-                "reg2aln": "k_r2a_key+sort+k_reg2aln_g16+g32+w"}
+                "reg2aln": "k_r2a_key+sort+k_reg2aln_diag+g16+g32+w"}
 # per-launch HBM traffic from the committed PMC passes (tools/profile_round.sh + tools/traffic_from_pmc.py,
 # FETCH_SIZE corrected by the calib_fetch.hip gather calibration); PMC cannot be collected in-process
 TRAFFIC_JSON = {"c3": os.path.join(ROOT, "profiles", "traffic.json"),
@@ -515,6 +515,8 @@ def main() -> int:
     ap.add_argument("--group-devices", default=None,
                     help="in-process group (--gpus N without torchrun): comma-separated device of each member "
                          "(default 0..N-1; a repeated device makes replicas on one GPU, for tests)")
+    ap.add_argument("--cursor-only", action="store_true",
+                    help="after the timed steps, only the pipelined cursor measurement (profiling the drop-in loop)")
     ap.add_argument("--cursor-depth", type=int, default=8,
                     help="fetches in flight in the sql_cursor measurement (BwaIndex::pipeline_depth's default)")
     ap.add_argument("--seed-offset", type=int, default=0,
@@ -524,6 +526,8 @@ def main() -> int:
                     help="add the oracle-format checksum of every rank/member's full read set to the line")
     args = ap.parse_args()
     if args.timed_only:
+        args.no_cpu_baseline = args.no_codec = args.no_isolated = True
+    if args.cursor_only:
         args.no_cpu_baseline = args.no_codec = args.no_isolated = True
     cfg = CONFIGS[args.config]
     args.reads = args.reads or cfg["reads"]
@@ -770,84 +774,85 @@ def main() -> int:
 
     # ---- host materialisation: the last step's rows rendered as bwa_result text ----
     if rank == 0 and not cfg["seeding"] and n_hits and not args.timed_only:
-        hb.phase = "rendering rows on the host"
         keep, ptrs = reads_as_nuclseq(L, reads)
-        base = ctypes.addressof(ptrs)
-        sub_ptrs = [ctypes.cast(base + lo_k[k] * ctypes.sizeof(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
-                    for k in range(S)]   # sub-batch k's reads (its read_index is local)
+        if not args.cursor_only:
+            hb.phase = "rendering rows on the host"
+            base = ctypes.addressof(ptrs)
+            sub_ptrs = [ctypes.cast(base + lo_k[k] * ctypes.sizeof(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
+                        for k in range(S)]   # sub-batch k's reads (its read_index is local)
 
-        def host_render():
-            n = 0
-            for k, b in enumerate(batches):
-                p = L.bsq_render_tsv(idx, L.bsq_batch_hits(b), sub_ptrs[k])
-                n += len(ctypes.string_at(p)) if p else 0
-                L.bsq_free(p)
-            return n
+            def host_render():
+                n = 0
+                for k, b in enumerate(batches):
+                    p = L.bsq_render_tsv(idx, L.bsq_batch_hits(b), sub_ptrs[k])
+                    n += len(ctypes.string_at(p)) if p else 0
+                    L.bsq_free(p)
+                return n
 
-        def gpu_render():
-            n = 0
-            tt, tn = ctypes.c_void_p(), ctypes.c_int64()
-            for k, b in enumerate(batches):
-                N.check(L.bsq_batch_render(b, sub_ptrs[k], ctypes.byref(tt), ctypes.byref(tn)))
-                n += int(tn.value)
-            return n
+            def gpu_render():
+                n = 0
+                tt, tn = ctypes.c_void_p(), ctypes.c_int64()
+                for k, b in enumerate(batches):
+                    N.check(L.bsq_batch_render(b, sub_ptrs[k], ctypes.byref(tt), ctypes.byref(tn)))
+                    n += int(tn.value)
+                return n
 
-        t1 = time.perf_counter()
-        nbytes = host_render()
-        dt_r = time.perf_counter() - t1
-        os.environ["BSQ_RENDER_THREADS"] = "1"   # the reference's single-backend rendering, for comparison
-        t1 = time.perf_counter()
-        host_render()
-        dt_1 = time.perf_counter() - t1
-        del os.environ["BSQ_RENDER_THREADS"]
-        gpu_render()   # warm (buffers)
-        t1 = time.perf_counter()
-        gbytes = gpu_render()
-        dt_g = time.perf_counter() - t1
-        result["gpu_render"] = {"rows": n_hits, "seconds": round(dt_g, 4), "rows_per_s": round(n_hits / dt_g, 1),
-                                "text_MB": round(gbytes / 1e6, 1), "same_bytes_as_host": gbytes == nbytes,
-                                "note": "bsq_batch_render: rows rendered on the GPU incl. record upload and text D2H"}
+            t1 = time.perf_counter()
+            nbytes = host_render()
+            dt_r = time.perf_counter() - t1
+            os.environ["BSQ_RENDER_THREADS"] = "1"   # the reference's single-backend rendering, for comparison
+            t1 = time.perf_counter()
+            host_render()
+            dt_1 = time.perf_counter() - t1
+            del os.environ["BSQ_RENDER_THREADS"]
+            gpu_render()   # warm (buffers)
+            t1 = time.perf_counter()
+            gbytes = gpu_render()
+            dt_g = time.perf_counter() - t1
+            result["gpu_render"] = {"rows": n_hits, "seconds": round(dt_g, 4), "rows_per_s": round(n_hits / dt_g, 1),
+                                    "text_MB": round(gbytes / 1e6, 1), "same_bytes_as_host": gbytes == nbytes,
+                                    "note": "bsq_batch_render: rows rendered on the GPU incl. record upload and text D2H"}
 
-        def gpu_columns():   # build_tuple_bwa's two nuclseq columns per row (bsq_batch_render_nuclseqs)
-            out, oo = ctypes.c_void_p(), ctypes.c_void_p()
-            for k, b in enumerate(batches):
-                N.check(L.bsq_batch_render_nuclseqs(b, sub_ptrs[k], ctypes.byref(out), ctypes.byref(oo)))
-                L.bsq_free(out)
-                L.bsq_free(oo)
+            def gpu_columns():   # build_tuple_bwa's two nuclseq columns per row (bsq_batch_render_nuclseqs)
+                out, oo = ctypes.c_void_p(), ctypes.c_void_p()
+                for k, b in enumerate(batches):
+                    N.check(L.bsq_batch_render_nuclseqs(b, sub_ptrs[k], ctypes.byref(out), ctypes.byref(oo)))
+                    L.bsq_free(out)
+                    L.bsq_free(oo)
 
-        gpu_columns()   # warm
-        t1 = time.perf_counter()
-        gpu_columns()
-        result["gpu_render"]["nuclseq_columns_rows_per_s"] = round(n_hits / (time.perf_counter() - t1), 1)
-        result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
-                                 "rows_per_s_1thread": round(n_hits / dt_1, 1),
-                                 "text_MB": round(nbytes / 1e6, 1), "threads": min(16, host_cpus()["usable"]),
-                                 "note": "bsq_render_tsv of the last step (BwaMatch text, Q3/Q7/Q8 rules); "
-                                         "outside the timed region"}
-        # the SQL-level call: one bsq_align_batch over the cursor's nuclseq values in
-        # host memory -- batch and workspace set-up, device nt4 conversion, alignment, record copy
-        hb.phase = "one-shot bsq_align_batch"
-        ho = ctypes.POINTER(N.Hits)()
-        t1 = time.perf_counter()
-        N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
-        dt_s = time.perf_counter() - t1
-        dts = []
-        for _ in range(3):   # later calls reuse the index's pipeline (workspaces kept) and result arrays
-            L.bsq_hits_free(ho)
+            gpu_columns()   # warm
+            t1 = time.perf_counter()
+            gpu_columns()
+            result["gpu_render"]["nuclseq_columns_rows_per_s"] = round(n_hits / (time.perf_counter() - t1), 1)
+            result["host_render"] = {"rows": n_hits, "seconds": round(dt_r, 3), "rows_per_s": round(n_hits / dt_r, 1),
+                                     "rows_per_s_1thread": round(n_hits / dt_1, 1),
+                                     "text_MB": round(nbytes / 1e6, 1), "threads": min(16, host_cpus()["usable"]),
+                                     "note": "bsq_render_tsv of the last step (BwaMatch text, Q3/Q7/Q8 rules); "
+                                             "outside the timed region"}
+            # the SQL-level call: one bsq_align_batch over the cursor's nuclseq values in
+            # host memory -- batch and workspace set-up, device nt4 conversion, alignment, record copy
+            hb.phase = "one-shot bsq_align_batch"
             ho = ctypes.POINTER(N.Hits)()
             t1 = time.perf_counter()
             N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
-            dts.append(time.perf_counter() - t1)
-        dt_s2 = sorted(dts)[1]
-        result["sql_batch_call"] = {
-            "reads": reads.n, "seconds": round(dt_s, 3), "reads_per_s": round(reads.n / dt_s, 1),
-            "repeat_call_s": [round(x, 4) for x in dts], "repeat_call_reads_per_s": round(reads.n / dt_s2, 1),
-            "same_rows": int(ho.contents.n_hits) == n_hits,
-            "note": "bsq_align_batch from nuclseq varlenas in host memory, one call (staging, upload, device nt4 "
-                    "conversion, alignment as concurrent shares, D2H, merged result arrays); first call includes "
-                    "workspace allocation; repeat = median of 3"}
-        L.bsq_hits_free(ho)
-        N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
+            dt_s = time.perf_counter() - t1
+            dts = []
+            for _ in range(3):   # later calls reuse the index's pipeline (workspaces kept) and result arrays
+                L.bsq_hits_free(ho)
+                ho = ctypes.POINTER(N.Hits)()
+                t1 = time.perf_counter()
+                N.check(L.bsq_align_batch(idx, ctypes.byref(opts), ptrs, reads.n, first_call, ctypes.byref(ho)))
+                dts.append(time.perf_counter() - t1)
+            dt_s2 = sorted(dts)[1]
+            result["sql_batch_call"] = {
+                "reads": reads.n, "seconds": round(dt_s, 3), "reads_per_s": round(reads.n / dt_s, 1),
+                "repeat_call_s": [round(x, 4) for x in dts], "repeat_call_reads_per_s": round(reads.n / dt_s2, 1),
+                "same_rows": int(ho.contents.n_hits) == n_hits,
+                "note": "bsq_align_batch from nuclseq varlenas in host memory, one call (staging, upload, device nt4 "
+                        "conversion, alignment as concurrent shares, D2H, merged result arrays); first call includes "
+                        "workspace allocation; repeat = median of 3"}
+            L.bsq_hits_free(ho)
+            N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
 
         # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
         # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (8) (each fetch staged, then its tuples released),

@@ -70,6 +70,7 @@ struct RenderView {
 hipError_t launch_row_len(hipStream_t, const RenderView &, int64_t *);
 hipError_t launch_row_write(hipStream_t, const RenderView &, const int64_t *, char *);
 hipError_t launch_sub_write(hipStream_t, const RenderView &, const int64_t *, char *);
+hipError_t launch_col_lens(hipStream_t, const RenderView &, int64_t *, int64_t *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
 hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *, int);
@@ -79,10 +80,11 @@ hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *
 // codec_gpu.hip
 struct EncView { const uint8_t *text; const int64_t *toff; const int64_t *poff; int64_t n, slots; int validate; };
 struct DecView { const uint8_t *in; const int64_t *in_off; const int64_t *poff; const int64_t *toff; int64_t n, slots; };
-hipError_t launch_enc_count(hipStream_t, const EncView &, int64_t, int64_t *, int64_t *, uint32_t *, unsigned long long *);
+hipError_t launch_enc_count(hipStream_t, const EncView &, int64_t, int64_t *, int64_t *, int64_t *, uint32_t *,
+                            unsigned long long *);
 hipError_t launch_enc_meta(hipStream_t, const EncView &, const int64_t *, const int64_t *, int64_t, const uint32_t *,
                            int64_t *, int64_t *, int64_t *);
-hipError_t launch_enc_write(hipStream_t, const EncView &, int64_t, const int64_t *, const int64_t *, const int64_t *,
+hipError_t launch_enc_write(hipStream_t, const EncView &, int64_t, const int64_t *, const int64_t *, const int64_t *, const int64_t *,
                             const int64_t *, const int64_t *, int64_t, uint8_t *);
 hipError_t launch_dec(hipStream_t, const DecView &, const int64_t *, int64_t, char *);
 hipError_t launch_dec_codes(hipStream_t, const DecView &, const int64_t *, int64_t, uint8_t *);
@@ -1256,6 +1258,12 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
                                     w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
                                     w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr,
                                     r_order && !no_r2a_diag() ? w.eidx0 : nullptr));
+        if (getenv("BSQ_R2A_COUNTS")) {   // diagnostics: reads handed on by each reg2aln kernel (host sync)
+            int32_t dc[4] = {0, 0, 0, 0};
+            HIPCHK(hipMemcpyAsync(dc, w.dcount, sizeof dc, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            fprintf(stderr, "bsq_r2a reads %d: to g16 %d, to g32 %d, to w %d\n", n, dc[3], dc[0], dc[1]);
+        }
     } else {
         HIPCHK(launch_reg2aln(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.regs, w.n_regs, w.hits, w.cigars,
                               w.n_cig, w.status, w.scratch, b->ctr));
@@ -2135,18 +2143,18 @@ int codec_device(int device)
 // nuclseq_from_text of n texts already in HBM (text i at d_text + toff[i], pac bytes poff[]): the varlenas
 // are written to *d_out at the device offsets *d_off (n+1, 8-byte aligned), *total bytes.  With validate,
 // a character nuclseq_in rejects stops before the write pass: *first_bad = its text offset (else ~0).
+// d_toff / d_poff: the texts' offsets and pac-byte offsets (n + 1 each) already on the device; slots = d_poff[n].
 template <class Alloc>
-static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const std::vector<int64_t> &toff,
-                         const std::vector<int64_t> &poff, int64_t n, bool validate, uint8_t **d_out, int64_t **d_off,
-                         int64_t *total, unsigned long long *first_bad, double *kernel_ms)
+static int encode_device_core(hipStream_t st, Alloc &da, const uint8_t *d_text, const int64_t *d_toff,
+                              const int64_t *d_poff, int64_t slots, int64_t n, bool validate, uint8_t **d_out,
+                              int64_t **d_off, int64_t *total, unsigned long long *first_bad, double *kernel_ms)
 {
-    const int64_t slots = poff[(size_t)n], ntiles = (slots + 255) / 256;
+    const int64_t ntiles = (slots + 255) / 256;
     if (ntiles + 1 >= INT32_MAX || n + 1 >= INT32_MAX) { set_err("batch too large (%lld pac bytes)", (long long)slots); return BSQ_E_INVALID; }
-    int64_t *d_toff, *d_poff, *tile_hb, *tile_hs, *hb_base, *hs_base, *off;
+    int64_t *tile_first, *tile_hb, *tile_hs, *hb_base, *hs_base, *off;
     uint32_t *loc;
     unsigned long long *bad;
-    HIPCHK(da.get(d_toff, (size_t)n + 1));
-    HIPCHK(da.get(d_poff, (size_t)n + 1));
+    HIPCHK(da.get(tile_first, (size_t)ntiles + 1));
     HIPCHK(da.get(tile_hb, (size_t)ntiles + 1));
     HIPCHK(da.get(tile_hs, (size_t)ntiles + 1));
     HIPCHK(da.get(hb_base, (size_t)n + 1));
@@ -2154,8 +2162,6 @@ static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const
     HIPCHK(da.get(off, (size_t)n + 1));
     HIPCHK(da.get(loc, (size_t)n + 1));
     HIPCHK(da.get(bad, 1));
-    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(tile_hb, 0, ((size_t)ntiles + 1) * 8, st));
     HIPCHK(hipMemsetAsync(tile_hs, 0, ((size_t)ntiles + 1) * 8, st));
     HIPCHK(hipMemsetAsync(bad, 0xff, 8, st));
@@ -2164,7 +2170,7 @@ static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const
     struct EvFree { hipEvent_t *e; ~EvFree() { for (int i = 0; i < 4; ++i) hipEventDestroy(e[i]); } } evf{ev};
     const EncView v{d_text, d_toff, d_poff, n, slots, validate ? 1 : 0};
     HIPCHK(hipEventRecord(ev[0], st));
-    HIPCHK(launch_enc_count(st, v, ntiles, tile_hb, tile_hs, loc, bad));
+    HIPCHK(launch_enc_count(st, v, ntiles, tile_first, tile_hb, tile_hs, loc, bad));
     size_t tb = 0, tb2 = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_hb, tile_hb, (int)(ntiles + 1), st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, off, off, (int)(n + 1), st));
@@ -2186,7 +2192,7 @@ static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const
     uint8_t *out;
     HIPCHK(da.get(out, (size_t)tot[0]));
     HIPCHK(hipEventRecord(ev[2], st));
-    HIPCHK(launch_enc_write(st, v, ntiles, tile_hb, tile_hs, hb_base, hs_base, off, tot[1], out));
+    HIPCHK(launch_enc_write(st, v, ntiles, tile_first, tile_hb, tile_hs, hb_base, hs_base, off, tot[1], out));
     HIPCHK(hipEventRecord(ev[3], st));
     HIPCHK(hipStreamSynchronize(st));
     float a = 0, c = 0;
@@ -2195,6 +2201,21 @@ static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const
     *kernel_ms = a + c;
     *d_out = out;
     return BSQ_OK;
+}
+
+// the same with the offsets in host vectors (uploaded first)
+template <class Alloc>
+static int encode_device(hipStream_t st, Alloc &da, const uint8_t *d_text, const std::vector<int64_t> &toff,
+                         const std::vector<int64_t> &poff, int64_t n, bool validate, uint8_t **d_out, int64_t **d_off,
+                         int64_t *total, unsigned long long *first_bad, double *kernel_ms)
+{
+    int64_t *d_toff, *d_poff;
+    HIPCHK(da.get(d_toff, (size_t)n + 1));
+    HIPCHK(da.get(d_poff, (size_t)n + 1));
+    HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+    return encode_device_core(st, da, d_text, d_toff, d_poff, poff[(size_t)n], n, validate, d_out, d_off, total,
+                              first_bad, kernel_ms);
 }
 
 // copies n+1 offsets and the bytes they span from the device into malloc'd host arrays
@@ -2290,33 +2311,41 @@ int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **ou
         }
     }
     hipStream_t st = b->cstream;
-    std::vector<int64_t> toff((size_t)n + 1, 0), poff((size_t)n + 1, 0);
+    // text and pac-byte totals from the host view; the per-text offsets are computed on the device from the records
+    int64_t text_total = 0, slots = 0;
     for (int64_t k = 0; k < H.n_hits; ++k) {
         const bsq_hit &x = H.hits[k];
-        const int64_t l[2] = {x.re - x.rb, (int64_t)x.qe - x.qb};
-        for (int t = 0; t < 2; ++t) {
-            const size_t i = (size_t)(2 * k + t);
-            toff[i + 1] = toff[i] + l[t];
-            poff[i + 1] = poff[i] + (l[t] + 3) / 4;
-        }
+        const int64_t l0 = x.re - x.rb, l1 = (int64_t)x.qe - x.qb;
+        text_total += l0 + l1;
+        slots += ((l0 + 3) >> 2) + ((l1 + 3) >> 2);
     }
     b->arena.reset();
     char *d_text;
-    int64_t *d_toff;
-    HIPCHK(b->arena.get(d_text, (size_t)toff[(size_t)n]));
+    int64_t *d_toff, *d_poff;
+    HIPCHK(b->arena.get(d_text, (size_t)text_total));
     HIPCHK(b->arena.get(d_toff, (size_t)n + 1));
+    HIPCHK(b->arena.get(d_poff, (size_t)n + 1));
     if (H.n_hits) {
         RenderView v{};
         { const int rc = render_inputs(b, reads, v, st); if (rc) return rc; }
-        HIPCHK(hipMemcpyAsync(d_toff, toff.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_col_lens(st, v, d_toff, d_poff));
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_toff, d_toff, (int)(n + 1), st));
+        uint8_t *cub = nullptr;
+        HIPCHK(b->arena.get(cub, tb));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_toff, d_toff, (int)(n + 1), st));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_poff, d_poff, (int)(n + 1), st));
         HIPCHK(launch_sub_write(st, v, d_toff, d_text));
+    } else {
+        HIPCHK(hipMemsetAsync(d_toff, 0, 8, st));
+        HIPCHK(hipMemsetAsync(d_poff, 0, 8, st));
     }
     uint8_t *d_out = nullptr;
     int64_t *d_off = nullptr, total = 0;
     unsigned long long first_bad = ~0ull;
     double kms = 0;
-    { const int rc = encode_device(st, b->arena, reinterpret_cast<const uint8_t *>(d_text), toff, poff, n, false, &d_out,
-                                   &d_off, &total, &first_bad, &kms);
+    { const int rc = encode_device_core(st, b->arena, reinterpret_cast<const uint8_t *>(d_text), d_toff, d_poff, slots, n,
+                                        false, &d_out, &d_off, &total, &first_bad, &kms);
       if (rc) return rc; }
     { int rc = grow_pinned(b->c_host, b->c_host_cap, std::max<int64_t>(total, 1), 0); if (rc) return rc; }
     { int rc = grow_pinned(b->c_off, b->c_off_cap, n + 1, 0); if (rc) return rc; }

@@ -86,18 +86,22 @@ DEV int64_t text_of(const int64_t *poff, int64_t g, int64_t lo, int64_t hi)
     return lo;
 }
 
-// the tile's first and last text, found once per block
-DEV void tile_texts(const EncView &v, int64_t tile, int64_t &s_lo, int64_t &s_hi)
+// tile_first[t] = the text holding pac byte t * CT (every tile start lies in exactly one text with bytes), so a tile
+// finds its texts with two loads instead of two binary searches by its first lane while the other 255 wait (a batch
+// of row columns holds ~2M texts of ~40 bytes: 21 dependent loads per tile before any lane could start)
+__global__ void k_enc_tiles(const int64_t *poff, int64_t n, int64_t ntiles, int64_t *tile_first)
 {
-    __shared__ int64_t sh[2];
-    if (threadIdx.x == 0) {
-        const int64_t g0 = tile * CT, g1 = (g0 + CT < v.slots ? g0 + CT : v.slots) - 1;
-        sh[0] = text_of(v.poff, g0, 0, v.n - 1);
-        sh[1] = text_of(v.poff, g1, sh[0], v.n - 1);
-    }
-    __syncthreads();
-    s_lo = sh[0]; s_hi = sh[1];
-    __syncthreads();
+    // one thread per tile (each search independent, all in flight at once: a few huge texts or millions of
+    // short ones alike)
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles; t += (int64_t)gridDim.x * blockDim.x)
+        tile_first[t] = t < ntiles ? text_of(poff, t * CT, 0, n - 1) : (n > 0 ? n - 1 : 0);
+}
+
+// the tile's first text and an upper bound of its last (the text holding the next tile's first byte)
+DEV void tile_texts(const int64_t *tile_first, int64_t tile, int64_t &s_lo, int64_t &s_hi)
+{
+    s_lo = tile_first[tile];
+    s_hi = tile_first[tile + 1];
 }
 
 // hole bases (low 16 bits) and hole starts (high 16 bits) among the lane's 4 bases
@@ -117,13 +121,13 @@ DEV uint32_t lane_counts(const EncView &v, int64_t s, int64_t i0, unsigned long 
 
 using TileScan = hipcub::BlockScan<uint32_t, CT>;
 
-__global__ __launch_bounds__(CT) void k_enc_count(EncView v, int64_t ntiles, int64_t *tile_hb, int64_t *tile_hs,
-                                                  uint32_t *loc, unsigned long long *bad)
+__global__ __launch_bounds__(CT) void k_enc_count(EncView v, int64_t ntiles, const int64_t *tile_first, int64_t *tile_hb,
+                                                  int64_t *tile_hs, uint32_t *loc, unsigned long long *bad)
 {
     __shared__ typename TileScan::TempStorage ts;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         int64_t s_lo, s_hi;
-        tile_texts(v, tile, s_lo, s_hi);
+        tile_texts(tile_first, tile, s_lo, s_hi);
         const int64_t g = tile * CT + threadIdx.x;
         uint32_t cnt = 0;
         int64_t s = -1, i0 = 0;
@@ -172,14 +176,14 @@ __global__ void k_enc_size(EncView v, const int64_t *hs_base, int64_t *size)
 DEV void st32(uint8_t *p, uint32_t x) { *reinterpret_cast<uint32_t *>(p) = x; }   // 4-byte aligned
 DEV uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
 
-__global__ __launch_bounds__(CT) void k_enc_write(EncView v, int64_t ntiles, const int64_t *tile_hb,
-                                                  const int64_t *tile_hs, const int64_t *hb_base,
+__global__ __launch_bounds__(CT) void k_enc_write(EncView v, int64_t ntiles, const int64_t *tile_first,
+                                                  const int64_t *tile_hb, const int64_t *tile_hs, const int64_t *hb_base,
                                                   const int64_t *hs_base, const int64_t *out_off, uint8_t *out)
 {
     __shared__ typename TileScan::TempStorage ts;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         int64_t s_lo, s_hi;
-        tile_texts(v, tile, s_lo, s_hi);
+        tile_texts(tile_first, tile, s_lo, s_hi);
         const int64_t g = tile * CT + threadIdx.x;
         uint32_t cnt = 0;
         int64_t s = -1, i0 = 0;
@@ -263,10 +267,15 @@ inline dim3 cgrid(int64_t n, int per = 256)
     return dim3((unsigned)(b < (1 << 20) ? (b ? b : 1) : (1 << 20)));
 }
 
-hipError_t launch_enc_count(hipStream_t st, const EncView &v, int64_t ntiles, int64_t *tile_hb, int64_t *tile_hs,
-                            uint32_t *loc, unsigned long long *bad)
+// tile_first: ntiles + 1 entries of scratch, filled here and read again by launch_enc_write
+hipError_t launch_enc_count(hipStream_t st, const EncView &v, int64_t ntiles, int64_t *tile_first, int64_t *tile_hb,
+                            int64_t *tile_hs, uint32_t *loc, unsigned long long *bad)
 {
-    if (ntiles) hipLaunchKernelGGL(k_enc_count, cgrid(ntiles, 1), dim3(CT), 0, st, v, ntiles, tile_hb, tile_hs, loc, bad);
+    if (ntiles) {
+        hipLaunchKernelGGL(k_enc_tiles, cgrid(ntiles + 1), dim3(256), 0, st, v.poff, v.n, ntiles, tile_first);
+        hipLaunchKernelGGL(k_enc_count, cgrid(ntiles, 1), dim3(CT), 0, st, v, ntiles, tile_first, tile_hb, tile_hs,
+                           loc, bad);
+    }
     return hipGetLastError();
 }
 
@@ -278,13 +287,13 @@ hipError_t launch_enc_meta(hipStream_t st, const EncView &v, const int64_t *tile
     return hipGetLastError();
 }
 
-hipError_t launch_enc_write(hipStream_t st, const EncView &v, int64_t ntiles, const int64_t *tile_hb,
-                            const int64_t *tile_hs, const int64_t *hb_base, const int64_t *hs_base,
-                            const int64_t *out_off, int64_t n_holes, uint8_t *out)
+hipError_t launch_enc_write(hipStream_t st, const EncView &v, int64_t ntiles, const int64_t *tile_first,
+                            const int64_t *tile_hb, const int64_t *tile_hs, const int64_t *hb_base,
+                            const int64_t *hs_base, const int64_t *out_off, int64_t n_holes, uint8_t *out)
 {
     if (ntiles)
-        hipLaunchKernelGGL(k_enc_write, cgrid(ntiles, 1), dim3(CT), 0, st, v, ntiles, tile_hb, tile_hs, hb_base,
-                           hs_base, out_off, out);
+        hipLaunchKernelGGL(k_enc_write, cgrid(ntiles, 1), dim3(CT), 0, st, v, ntiles, tile_first, tile_hb, tile_hs,
+                           hb_base, hs_base, out_off, out);
     if (v.n) hipLaunchKernelGGL(k_enc_header, cgrid(v.n), dim3(256), 0, st, v, hs_base, out_off, out);
     if (n_holes) hipLaunchKernelGGL(k_enc_holes, cgrid(n_holes), dim3(256), 0, st, v, hs_base, n_holes, out_off, out);
     return hipGetLastError();
@@ -317,6 +326,29 @@ __global__ void k_dec_bases(DecView v, char *out)
     }
 }
 
+// Short texts (reads: ~38 pac bytes): one lane per text walks its pac words -- k_dec_bases' per-byte lanes each
+// binary-search the text over all n (18 dependent loads per byte for a 262k-read fetch).  The pac bytes start 4-byte
+// aligned (8-aligned varlena + 12 + 16 per hole).
+template <bool CODES>
+__global__ void k_dec_bases_lane(DecView v, char *out)
+{
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < v.n; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t *ns = v.in + v.in_off[s];
+        const uint32_t nh = ld32(ns + 4);
+        const int64_t len = v.toff[s + 1] - v.toff[s];
+        const uint8_t *pac = ns + 12 + 16 * (int64_t)nh;
+        char *o = out + v.toff[s];
+        for (int64_t i = 0; i < len; i += 16) {
+            const uint32_t w = ld32(pac + (i >> 2));   // bytes i/4 .. i/4+3: bases i .. i+15, first byte lowest
+            const int m = len - i < 16 ? (int)(len - i) : 16;
+            for (int k = 0; k < m; ++k) {
+                const uint32_t c = (w >> (((k >> 2) << 3) + ((3 - (k & 3)) << 1))) & 3;
+                o[i + k] = CODES ? (char)c : "ACGT"[c];
+            }
+        }
+    }
+}
+
 // one block per text with holes: holes in order, later ones overwrite (inplace_to_text :77-78); as nt4
 // codes every hole base is 4 (ns_to_nt4: hole symbols are never ACGT)
 template <bool CODES>
@@ -341,7 +373,8 @@ __global__ void k_dec_holes(DecView v, const int64_t *texts, char *out)
 template <bool CODES>
 static hipError_t dec(hipStream_t st, const DecView &v, const int64_t *hole_texts, int64_t n_hole_texts, char *out)
 {
-    if (v.slots) hipLaunchKernelGGL(k_dec_bases<CODES>, cgrid(v.slots), dim3(256), 0, st, v, out);
+    if (v.slots && v.slots <= 64 * v.n) hipLaunchKernelGGL(k_dec_bases_lane<CODES>, cgrid(v.n), dim3(256), 0, st, v, out);
+    else if (v.slots) hipLaunchKernelGGL(k_dec_bases<CODES>, cgrid(v.slots), dim3(256), 0, st, v, out);
     for (int64_t k = 0; k < n_hole_texts; k += 65535)   // one block per text with holes
         hipLaunchKernelGGL(k_dec_holes<CODES>, dim3((unsigned)(n_hole_texts - k < 65535 ? n_hole_texts - k : 65535)),
                            dim3(256), 0, st, v, hole_texts + k, out);

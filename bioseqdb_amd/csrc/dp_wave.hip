@@ -907,6 +907,32 @@ DEV bool diag_decides(const DIndex &ix, const DOpts &o, const Score sc, int w_, 
     return (int64_t)sum > bound2 && (int64_t)x < (int64_t)(o.o_ins + o.e_ins + o.o_del + o.e_del);
 }
 
+// mem_reg2aln's first band of a region as k_r2a_key classes it: 1 (<= 16 columns), 2 (<= 32) or 3 (wider)
+DEV int band_class(const DOpts &o, int lq, int64_t rl, int w2)
+{
+    if (lq <= 0 || rl <= 0 || rl > (1 << 30)) return 1;   // gen_cigar2's early exits: no DP in any kernel
+    int mg = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
+    int md = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
+    mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
+    int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
+    int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
+    const int nc = lq < 2 * ww + 1 ? lq : 2 * ww + 1;
+    return nc <= 16 ? 1 : nc <= 32 ? 2 : 3;
+}
+
+// appends li (when `on`) to list/count in lane order: one atomic per wave
+DEV void wave_append(bool on, int li, int32_t *list, int32_t *count)
+{
+    const uint64_t m = __ballot(on);
+    int base = 0;
+    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (on) list[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = li;
+}
+
+// Reads with a region the pass does not decide go straight to the kernel of their widest first band (the class
+// k_r2a_key sorts by): <= 16 columns to `defer` (k_reg2aln_g<16>'s input), <= 32 to d0 (k_reg2aln_g<32>'s), wider
+// to d1 (k_reg2aln_w's) -- each kernel recomputes a read from scratch and still defers what outgrows it.
 __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps cp, const uint8_t *__restrict__ codes,
                                                       const int64_t *__restrict__ offs, int n,
                                                       const int32_t *__restrict__ list, const int32_t *__restrict__ list_n,
@@ -914,12 +940,13 @@ __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps c
                                                       Hit *__restrict__ hits, uint32_t *__restrict__ cigars,
                                                       int32_t *__restrict__ n_cig_read, const uint32_t *__restrict__ status,
                                                       int32_t *__restrict__ defer, int32_t *__restrict__ defer_n,
-                                                      Counters *ctr)
+                                                      int32_t *__restrict__ d0, int32_t *__restrict__ d1,
+                                                      int32_t *__restrict__ dn, Counters *ctr)
 {
     const int n_items = list ? *list_n : n;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int li = k < n_items ? (list ? list[k] : k) : -1;
-    bool dfr = false;
+    int cls = 0;   // widest first-band class among the regions the pass leaves to the DP kernels
     uint64_t bases = 0;
     if (li >= 0) {
         if (status[li]) n_cig_read[li] = 0;
@@ -929,23 +956,34 @@ __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps c
             const int nr = n_regs[li];
             const Score sc = score_of(o);
             int tot = 0;
-            dfr = cp.cigar < 3;   // "nM" plus two clips; smaller CIGAR slots take the group kernel's overflow path
-            for (int g = 0; g < nr && !dfr; ++g) {
+            bool dfr = cp.cigar < 3;   // "nM" plus two clips; smaller CIGAR slots take the group kernel's overflow path
+            if (dfr) cls = 1;
+            for (int g = 0; g < nr; ++g) {
                 const Reg &ar = regs[(size_t)li * cp.regs + g];
                 const int qb = ar.qb, qe = ar.qe, lq = qe - qb;
                 const int64_t rb = ar.rb, re = ar.re, rlen = re - rb;
-                // gen_cigar2_g's early exits and the DP case belong to the group kernel
-                if (lq <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac) || re > (ix.l_pac << 1) || rb < 0 ||
-                    rlen != lq) { dfr = true; break; }
                 int tmp = infer_bw(lq, (int)rlen, ar.truesc, o.a, o.o_del, o.e_del);
                 int w2 = infer_bw(lq, (int)rlen, ar.truesc, o.a, o.o_ins, o.e_ins);
                 w2 = w2 > tmp ? w2 : tmp;
                 if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
                 w2 = w2 < o.w << 2 ? w2 : o.w << 2;
+                if (dfr) {   // a region already left to the DP kernels: only the class of the rest matters
+                    const int c = band_class(o, lq, rlen, w2);
+                    cls = cls > c ? cls : c;
+                    continue;
+                }
+                // gen_cigar2_g's early exits and the DP case belong to the group kernels
+                const bool odd = lq <= 0 || rb >= re || (rb < ix.l_pac && re > ix.l_pac) || re > (ix.l_pac << 1) || rb < 0;
                 const bool rev = rb >= ix.l_pac;
                 int S = 0;
-                if (!diag_decides(ix, o, sc, w2, codes, rd, l_read, rev ? qb + lq - 1 : qb, rev ? -1 : 1,
-                                  rev ? re - 1 : rb, rev ? -1 : 1, lq, S)) { dfr = true; break; }
+                if (odd || rlen != lq ||
+                    !diag_decides(ix, o, sc, w2, codes, rd, l_read, rev ? qb + lq - 1 : qb, rev ? -1 : 1,
+                                  rev ? re - 1 : rb, rev ? -1 : 1, lq, S)) {
+                    dfr = true;
+                    const int c = odd ? 1 : band_class(o, lq, rlen, w2);
+                    cls = cls > c ? cls : c;
+                    continue;
+                }
                 // the retry loop of k_reg2aln_g: a second call (doubled band) when the first band was not the
                 // widest and S < truesc - a; it decides the same way (the shortcut does not depend on w > 0)
                 bases += (uint64_t)((rlen + 3) >> 2);
@@ -968,12 +1006,10 @@ __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps c
             if (!dfr) n_cig_read[li] = tot;
         }
     }
-    // deferred reads keep their input order: one atomic per wave, lanes placed by the ballot's prefix
-    const uint64_t m = __ballot(dfr);
-    int base = 0;
-    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(defer_n, __popcll(m));
-    base = __shfl(base, 0, 64);
-    if (dfr) defer[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = li;
+    // the lists keep their input order within each (one atomic per wave and list)
+    wave_append(cls == 1, li, defer, defer_n);
+    wave_append(cls == 2, li, d0, dn);
+    wave_append(cls >= 3, li, d1, dn + 1);
     wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
 }
 
@@ -992,7 +1028,7 @@ hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o
         e = hipMemsetAsync(dn + 3, 0, sizeof(int32_t), st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_reg2aln_diag, dim3((n + 255) / 256), dim3(256), 0, st, ix, o, cp, codes, offs, n, order,
-                           order_n, regs, n_regs, hits, cigars, n_cig, status, pre, dn + 3, ctr);
+                           order_n, regs, n_regs, hits, cigars, n_cig, status, pre, dn + 3, d0, d1, dn, ctr);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         order = pre;

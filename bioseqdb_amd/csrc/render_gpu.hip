@@ -162,6 +162,25 @@ hipError_t launch_row_write(hipStream_t st, const RenderView &v, const int64_t *
     return hipGetLastError();
 }
 
+// lengths of the two subsequence texts of every row (text 2k: re - rb, text 2k+1: qe - qb) and their pac bytes,
+// with a 0 at [2 n_hits] so an exclusive scan of n + 1 entries gives the offsets and the totals
+__global__ void k_col_lens(const bsq_hit *hits, int64_t n_hits, int64_t *tl, int64_t *pl)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_hits; k += (int64_t)gridDim.x * blockDim.x) {
+        const bsq_hit x = hits[k];
+        const int64_t l0 = x.re - x.rb, l1 = (int64_t)x.qe - x.qb;
+        tl[2 * k] = l0; tl[2 * k + 1] = l1;
+        pl[2 * k] = (l0 + 3) >> 2; pl[2 * k + 1] = (l1 + 3) >> 2;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { tl[2 * n_hits] = 0; pl[2 * n_hits] = 0; }
+}
+
+hipError_t launch_col_lens(hipStream_t st, const RenderView &v, int64_t *tl, int64_t *pl)
+{
+    hipLaunchKernelGGL(k_col_lens, rgrid(v.n_hits), dim3(256), 0, st, v.hits, v.n_hits, tl, pl);
+    return hipGetLastError();
+}
+
 hipError_t launch_sub_write(hipStream_t st, const RenderView &v, const int64_t *toff, char *out)
 {
     hipLaunchKernelGGL(k_sub_write, rgrid(v.n_hits), dim3(256), 0, st, v, toff, out);
