@@ -515,6 +515,9 @@ def main() -> int:
     ap.add_argument("--group-devices", default=None,
                     help="in-process group (--gpus N without torchrun): comma-separated device of each member "
                          "(default 0..N-1; a repeated device makes replicas on one GPU, for tests)")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="a barrier after every timed step (bsq_batch_run_many per step) instead of one stream of "
+                         "batch runs over the K steps")
     ap.add_argument("--cursor-only", action="store_true",
                     help="after the timed steps, only the pipelined cursor measurement (profiling the drop-in loop)")
     ap.add_argument("--cursor-depth", type=int, default=8,
@@ -673,9 +676,17 @@ def main() -> int:
         import torch
         dist.barrier()
         torch.cuda.synchronize()
+    # Without a launcher the K steps run as one stream of batch runs (bsq_batch_run_rounds): each batch starts
+    # its next step as soon as its previous one ends, so one batch's seeding overlaps the others' DP tails
+    # instead of every step draining to a barrier; every step still aligns all the reads once, and the last
+    # step's records are checked below.  --lockstep: a barrier after every step (bsq_batch_run_many per step).
+    rounds = dist is None and S > 1 and not cfg["seeding"] and not args.lockstep
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if rounds:
+        N.check(L.bsq_batch_run_rounds(b_arr, S, ctypes.byref(opts), fc_arr, args.steps))
+    for _ in range(1 if rounds else args.steps):
+        if not rounds:
+            step()
         for b in batches:   # per-launch figures: averaged over the S concurrent launches of each stage
             ms = (ctypes.c_float * 6)()
             L.bsq_batch_stage_ms(b, ms, 6)
@@ -697,9 +708,9 @@ def main() -> int:
         t = torch.tensor([elapsed], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stage_ms /= max(args.steps, 1) * S
-    stage_bytes /= max(args.steps, 1) * S
-    stage_work /= max(args.steps, 1) * S
+    stage_ms /= (1 if rounds else max(args.steps, 1)) * S   # rounds: the last step's launches
+    stage_bytes /= (1 if rounds else max(args.steps, 1)) * S
+    stage_work /= (1 if rounds else max(args.steps, 1)) * S
     reads_per_launch = reads.n / S
     n_hits = sum(int(L.bsq_batch_hits(b).contents.n_hits) for b in batches) if not cfg["seeding"] else 0
     retried = sum(int(L.bsq_batch_retried(b)) for b in batches)
@@ -741,6 +752,8 @@ def main() -> int:
             "reads_per_gpu": args.reads, "read_len": args.read_len, "ref_bp": args.ref_bp,
             "parallelism": f"read-sharded x{world}" + (" (one process per GPU, RCCL record gather)" if world > 1 else ""),
             "hits_per_step_rank0": n_hits, "streams": S, "reads_per_launch": int(round(reads_per_launch)),
+            "step_schedule": ("stream of batch runs over the timed steps (bsq_batch_run_rounds; stage times of the "
+                              "last step)" if rounds else "barrier after every step"),
         },
         "exchange": None if xchg is None else {
             "path": ("RCCL gather of device records to rank 0, pinned D2H there, overlapped with the next step"

@@ -112,6 +112,8 @@ SIGNATURES = {
     "bsq_index_build_device": (ctypes.c_int, [_P, ctypes.c_int]),
     "bsq_batch_run_many": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(Opts),
                                           ctypes.POINTER(ctypes.c_uint64)]),
+    "bsq_batch_run_rounds": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(Opts),
+                                            ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "bsq_batch_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "bsq_index_download": (ctypes.c_int, [_P]),
     "bsq_index_build_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)]),

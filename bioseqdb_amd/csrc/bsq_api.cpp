@@ -1753,13 +1753,14 @@ extern "C" const bsq_hits *bsq_batch_hits(const bsq_batch *b) { return b ? &b->v
 // Several batches in flight at once, one host thread and one stream each: the stages of one batch fill
 // the tails and host gaps of the others (3 batches of 1/3 of the reads: +24 % reads/s at C3 on one
 // MI355X, whose process gets 4 hardware queues).  first_call[i] is batch i's lrand48 position.
-extern "C" int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call)
+extern "C" int bsq_batch_run_rounds(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call,
+                                    int rounds)
 {
-    if (n < 0 || (n > 0 && (!batches || !opts || !first_call))) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (n < 0 || rounds < 0 || (n > 0 && (!batches || !opts || !first_call))) { set_err("invalid argument"); return BSQ_E_INVALID; }
     std::vector<int> rc((size_t)n, BSQ_OK);
     std::vector<std::string> msg((size_t)n);
     auto one = [&](int i) {
-        rc[(size_t)i] = bsq_batch_run(batches[i], opts, first_call[i]);
+        for (int r = 0; r < rounds && !rc[(size_t)i]; ++r) rc[(size_t)i] = bsq_batch_run(batches[i], opts, first_call[i]);
         if (rc[(size_t)i]) msg[(size_t)i] = g_err;   // the message is thread-local: carry it to the caller
     };
     std::vector<std::thread> th;
@@ -1769,6 +1770,11 @@ extern "C" int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_op
     for (int i = 0; i < n; ++i)
         if (rc[(size_t)i]) { g_err = "batch " + std::to_string(i) + ": " + msg[(size_t)i]; return rc[(size_t)i]; }
     return BSQ_OK;
+}
+
+extern "C" int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call)
+{
+    return bsq_batch_run_rounds(batches, n, opts, first_call, 1);
 }
 
 // device buffer of at least `need` elements (contents not kept)

@@ -279,6 +279,13 @@ int bsq_batch_render_nuclseqs(bsq_batch *b, const void *const *reads, uint8_t **
  * first_call[i].  Each batch keeps its own result view.  Returns the first error, prefixed by the batch
  * index. */
 int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call);
+/* bsq_batch_run_many `rounds` times with no barrier between rounds: each batch's thread runs its batch again as
+ * soon as its previous run ends (a steady stream of cursor batches, extension.cpp:362-370 looped: one batch's
+ * next seeding overlaps the others' dynamic-programming tails).  Every round re-aligns the batch's reads from
+ * first_call[i], so the results equal one bsq_batch_run_many call's.  Stage times and bytes are the last
+ * round's. */
+int bsq_batch_run_rounds(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call,
+                         int rounds);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
 /* The last run's records as bytes in device memory on the batch's device: the bsq_hit array, then the CIGAR

@@ -56,6 +56,9 @@ def test_run_many_equals_one_batch(S):
             got = [r for k in range(S) for r in _rows(L, subs[k], lo[k])]
             assert len(got) == len(exp) and len(exp) > 5000
             assert got == exp
+        # bench.py's timed steps: three rounds with no barrier between them end with the same rows
+        N.check(L.bsq_batch_run_rounds(arr, S, ctypes.byref(pi.options), fc, 3))
+        assert [r for k in range(S) for r in _rows(L, subs[k], lo[k])] == exp
     finally:
         L.bsq_batch_free(whole)
         for b in subs:
