@@ -488,8 +488,8 @@ def run_group(args, cfg) -> int:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="c3 (default, the BASELINE metric), c2 (seeding only), c4 (3 Gbp reference)")
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU per step (default: the config's)")
