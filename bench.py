@@ -731,6 +731,9 @@ def main() -> int:
         iso = lone_launch(L, idx, opts, codes, offs, reads.n, first_call)
     elif S == 1:
         iso = (list(stage_ms), list(stage_bytes))
+    if iso:   # the dominant kernel by its own (lone) time: with steps as a stream, the batches' last-step stages
+        di = max(range(nst), key=lambda i: iso[0][i])   # overlap in whatever phase they drifted to
+        dom = names[di]
 
     total_reads = args.reads * world
     value = total_reads * args.steps / elapsed
