@@ -964,7 +964,8 @@ extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_b
     HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     for (auto &e : b->ev) HIPCHK(hipEventCreate(&e));
     const size_t R = (size_t)std::max(max_reads, 1);
-    HIPCHK(hipMalloc(&b->codes, (size_t)std::max<int64_t>(max_bases, 1)));
+    // whole 16-B words plus one: the reg2aln query stream loads the aligned word holding a read's last base
+    HIPCHK(hipMalloc(&b->codes, (size_t)((std::max<int64_t>(max_bases, 1) + 15) / 16 * 16 + 16)));
     HIPCHK(hipMalloc(&b->offs, (R + 1) * 8));
     HIPCHK(hipMalloc(&b->ids, R * 8));
     HIPCHK(hipMalloc(&b->ctr, sizeof(Counters) * STG_N));
@@ -1069,6 +1070,9 @@ int64_t batch_max_bases(const bsq_batch *b) { return b->max_bases; }
 int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
 {
     if (n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    // invalid until this staging succeeds: a RERUN of a failed staging must not find the old read count
+    s.n = -1;
+    s.host_bytes = 0;
     const size_t n = (size_t)n_reads;
     // Two passes over contiguous ranges of the reads, on up to 8 host threads for a large fetch (a cursor
     // fetch of 256k reads is ~13 MB of varlenas): sizes and offsets, then the copy into pinned memory.
@@ -1959,6 +1963,14 @@ void *out_alloc(size_t bytes)
     return static_cast<uint8_t *>(hdr) + kOutHdr;
 }
 
+void out_cache_drain()
+{
+    std::lock_guard<std::mutex> lk(g_out_mu);
+    for (auto &c : g_out_cache) free(c.second);
+    g_out_cache.clear();
+    g_out_bytes = 0;
+}
+
 void out_free(void *p)
 {
     if (!p) return;
@@ -2093,6 +2105,7 @@ extern "C" int bsq_index_release_pool(bsq_index *idx)
     if (!lk.owns_lock()) { set_err("the index's pooled pipeline is in use"); return BSQ_E_INVALID; }
     bsq_pipeline_free(idx->pipe);
     idx->pipe = nullptr;
+    out_cache_drain();   // the recycled result arrays of the one-shot calls (up to 2 GB) go back too
     return BSQ_OK;
 }
 

@@ -34,7 +34,7 @@ using namespace bsq;
 
 namespace {
 
-enum class SlotState { FREE, QUEUED, DONE, HELD };
+enum class SlotState { FREE, QUEUED, DONE, HELD };   // HELD: taken by the caller (or a failed take, below)
 
 struct Slot {
     SlotState state = SlotState::FREE;
@@ -54,6 +54,7 @@ struct Slot {
     // result
     int rc = BSQ_OK;
     std::string err;
+    bool failed_take = false;             // taken with an error: freed once every older taken slot is released
     const bsq_hits *view = nullptr;
     bsq_hits empty{};
     std::vector<int64_t> zeros;
@@ -101,6 +102,9 @@ void drop_cols(Slot &x)
 int prep_job(bsq_pipeline *p, Slot &x)
 {
     x.t[1] = now_ms();
+    if (const char *e = getenv("BSQ_PIPE_FAILPOINT")) {   // tests: job number e fails here (a failed fetch)
+        if (*e && strtoull(e, nullptr, 10) == x.job) { set_error("injected failure (BSQ_PIPE_FAILPOINT)"); return BSQ_E_INVALID; }
+    }
     if (x.mode == PipeMode::DEFER) {
         x.resident = false;
         const int rc = stage_nuclseqs(x.stage, x.reads, x.n);
@@ -199,6 +203,22 @@ int fail(int rc, const std::string &m)
     return rc;
 }
 
+// Free the oldest taken slots that were taken with an error (the caller never releases those).  Called with the
+// pipeline lock held.  A failed take behind a taken submission the caller still holds stays HELD until that one is
+// released, so a new submission can never land on a slot whose view the caller is still reading.
+void reap_failed(bsq_pipeline *p)
+{
+    while (p->n_release < p->n_take) {
+        Slot *y = p->s[p->n_release % p->s.size()].get();
+        if (!y->failed_take) break;
+        y->failed_take = false;
+        y->view = nullptr;
+        y->state = SlotState::FREE;
+        ++p->n_release;
+    }
+    p->cv.notify_all();
+}
+
 }  // namespace
 
 namespace bsq {
@@ -267,12 +287,13 @@ int pipeline_next_ex(bsq_pipeline *p, const bsq_hits **view, const uint8_t **col
         p->trace.push_back(r);
     }
     ++p->n_take;
-    if (x->rc) {   // consumed: the slot is free again (its submission produced no rows)
+    if (x->rc) {   // consumed: the slot is free again once every older taken submission is released
         const int rc = x->rc;
         const std::string m = x->err;
         x->state = SlotState::HELD;
-        lk.unlock();
-        bsq_pipeline_release(p);
+        x->failed_take = true;
+        drop_cols(*x);
+        reap_failed(p);
         return fail(rc, m);
     }
     x->state = SlotState::HELD;
@@ -354,6 +375,6 @@ extern "C" int bsq_pipeline_release(bsq_pipeline *p)
     x->view = nullptr;
     x->state = SlotState::FREE;
     ++p->n_release;
-    p->cv.notify_all();
+    reap_failed(p);
     return BSQ_OK;
 }

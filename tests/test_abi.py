@@ -107,3 +107,4 @@ def test_index_same_refs_built_vs_fresh():
         x.add_ref_sequence(7, NucleotideSequence.from_text("ACGTTGCANNGATTACA" * 40))
     a.build()
     assert L.bsq_index_same_refs(a.handle, b.handle) == 1
+

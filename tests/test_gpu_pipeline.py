@@ -145,6 +145,40 @@ def test_pipeline_full_and_empty(setup):
         L.bsq_pipeline_free(p)   # one submission still on the device: free waits for it
 
 
+
+def test_failed_take_behind_a_held_view(setup, monkeypatch):
+    """A fetch that fails while an older taken fetch is still held must not free the held slot: the next
+    submission would land on it and overwrite the rows the caller is reading.  The failure is
+    injected at job 1's staging (BSQ_PIPE_FAILPOINT); a 2-slot pipeline puts job 2 on job 0's slot."""
+    pi, seqs = setup
+    L = N.lib()
+    monkeypatch.setenv("BSQ_PIPE_FAILPOINT", "1")
+    ptrs = (ctypes.c_void_p * 50)(*[s.ptr for s in seqs[:50]])
+    p = ctypes.c_void_p()
+    N.check(L.bsq_pipeline_create(pi.handle, 2, ctypes.byref(p)))
+    try:
+        N.check(L.bsq_pipeline_submit(p, ctypes.byref(pi.options), ptrs, 50, 0, 0))    # job 0, slot 0
+        N.check(L.bsq_pipeline_submit(p, ctypes.byref(pi.options), ptrs, 50, 50, 0))   # job 1, slot 1: fails
+        v0 = ctypes.POINTER(N.Hits)()
+        N.check(L.bsq_pipeline_next(p, ctypes.byref(v0), None, None))
+        before = _records(v0.contents, 50)
+        v1 = ctypes.POINTER(N.Hits)()
+        assert L.bsq_pipeline_next(p, ctypes.byref(v1), None, None) == N.BSQ_E_INVALID
+        assert b"injected" in L.bsq_last_error()
+        # slot 0 is still the caller's: job 2 (slot 0 again) is refused and the held rows stay as they were
+        other = (ctypes.c_void_p * 25)(*[x.ptr for x in seqs[100:125]])
+        assert L.bsq_pipeline_submit(p, ctypes.byref(pi.options), other, 25, 100, 0) == N.BSQ_E_INVALID
+        assert _records(v0.contents, 50) == before
+        N.check(L.bsq_pipeline_release(p))   # frees slot 0 and, behind it, the failed slot 1
+        assert L.bsq_pipeline_release(p) == N.BSQ_E_INVALID
+        monkeypatch.delenv("BSQ_PIPE_FAILPOINT")
+        N.check(L.bsq_pipeline_submit(p, ctypes.byref(pi.options), ptrs, 50, 0, 0))
+        N.check(L.bsq_pipeline_next(p, ctypes.byref(v0), None, None))
+        assert _records(v0.contents, 50) == before   # the same fetch aligned again: the same rows
+        N.check(L.bsq_pipeline_release(p))
+    finally:
+        L.bsq_pipeline_free(p)
+
 def test_one_shot_split_does_not_change_rows(setup, monkeypatch):
     """bsq_align_batch over 1 slot vs 4 concurrent slots (24k reads -> shares of >= 32768 reads: one share;
     force small shares through BSQ_PIPE_SLOTS with a larger call): identical records."""
