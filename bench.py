@@ -18,16 +18,23 @@ N = 1 only; its outputs are also checksummed against the GPU's for the same read
 from __future__ import annotations
 
 import os
+import sys
 
 # HIP hardware queues of this process (the runtime's default is 4): the concurrent batches below each
 # own a stream, and 8 queues let 4 of them run without sharing a queue (+3 % over 3 batches on 4 queues).
-# Set before anything loads the HIP runtime (the box exports 4; BSQ_HW_QUEUES overrides this choice).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSQ_HW_QUEUES", "8")
+# RCCL communicators (a device group, the torchrun exchange lanes) take queues of their own: with 8, two batch
+# streams then share one and the step loses 15-20 % (one-device group at C3: 42.6 M reads/s on 8 queues, 49.4 M on
+# 16 -- the N = 1 line's rate).  Set before anything loads the HIP runtime (the box exports 4; BSQ_HW_QUEUES
+# overrides this choice).
+_RCCL_IN_PROCESS = (int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--exchange-world1" in sys.argv[1:]
+                    or "--group-devices" in sys.argv[1:]
+                    or any(a.startswith("--gpus") and (a.split("=")[1:] or ["1"])[0] != "1" for a in sys.argv[1:])
+                    or ("--gpus" in sys.argv[1:] and sys.argv[sys.argv.index("--gpus") + 1:][:1] != ["1"]))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSQ_HW_QUEUES", "16" if _RCCL_IN_PROCESS else "8")
 
 import argparse  # noqa: E402
 import ctypes  # noqa: E402
 import json  # noqa: E402
-import sys  # noqa: E402
 import time  # noqa: E402
 
 import numpy as np
@@ -81,6 +88,20 @@ class Heartbeat:
 
     def stop(self):
         self._stop.set()
+
+
+def json_out():
+    """The bench's stdout carries only its one JSON line: fd 1 is pointed at stderr for the rest of the process
+    (RCCL prints version banners on stdout when communicators initialise) and the line goes to a saved copy."""
+    global _OUT
+    if _OUT is None:
+        sys.stdout.flush()
+        _OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+    return _OUT
+
+
+_OUT = None
 
 
 def host_cpus() -> dict:
@@ -383,6 +404,8 @@ def run_group(args, cfg) -> int:
     darr = (ctypes.c_int * G)(*devs)
     N.check(L.bsq_group_create(darr, G, ctypes.byref(g)))
     N.check(L.bsq_group_set_slots(g, max(1, args.streams)))
+    via_first = args.exchange == "via-first"
+    N.check(L.bsq_group_set_exchange(g, 1 if via_first else 0))
     hb.phase = "replicating the index over the group"
     bc_ms = ctypes.c_double()
     N.check(L.bsq_group_replicate(g, idx, ctypes.byref(bc_ms)))
@@ -397,11 +420,16 @@ def run_group(args, cfg) -> int:
     first_call = args.seed_offset * args.reads
     hb.phase = "aligning"
     N.check(L.bsq_group_run(g, ctypes.byref(opts), ptrs, n_tot, first_call))   # stages every member's reads
-    for _ in range(max(args.warmup - 1, 0)):
-        N.check(L.bsq_group_run(g, ctypes.byref(opts), None, n_tot, first_call))
+    if args.warmup > 1:
+        N.check(L.bsq_group_run_rounds(g, ctypes.byref(opts), n_tot, first_call, args.warmup - 1))
+    # the timed steps: by default one stream of rounds per member (bsq_group_run_rounds: each share starts its next
+    # step as soon as its previous one is taken -- the N = 1 line's schedule); --lockstep: a group run per step
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        N.check(L.bsq_group_run(g, ctypes.byref(opts), None, n_tot, first_call))
+    if args.lockstep:
+        for _ in range(args.steps):
+            N.check(L.bsq_group_run(g, ctypes.byref(opts), None, n_tot, first_call))
+    else:
+        N.check(L.bsq_group_run_rounds(g, ctypes.byref(opts), n_tot, first_call, args.steps))
     elapsed = time.perf_counter() - t0
     t1 = time.perf_counter()
     H = L.bsq_group_hits(g)
@@ -423,9 +451,15 @@ def run_group(args, cfg) -> int:
                            "records to host memory over its own PCIe link)",
             "devices": devs, "distinct_devices": len(set(devs)), "shares_per_member": max(1, args.streams),
             "segments": n_seg, "hits_per_step": int(H.n_hits),
+            "step_schedule": ("barrier after every step (bsq_group_run per step)" if args.lockstep else
+                              "stream of rounds per member share over the timed steps (bsq_group_run_rounds)"),
         },
-        "exchange": {"path": "per-member pinned D2H inside the step (segments in read order); merged view after it",
-                     "merge_ms": round(merge_ms, 3), "broadcast_ms": round(bc_ms.value, 2)},
+        "exchange": {"path": ("members' records by peer DMA over xGMI into member 0's HBM, then member 0's PCIe D2H, "
+                              "inside the step (BSQ_XCHG_VIA_FIRST)" if via_first else
+                              "each member's records over its own PCIe link, pinned D2H inside the step "
+                              "(BSQ_XCHG_LINKS)") + "; segments in read order, merged view after the timed region",
+                     "mode": args.exchange, "merge_ms": round(merge_ms, 3), "broadcast_ms": round(bc_ms.value, 2),
+                     "record_bytes_per_step": int(H.n_hits) * ctypes.sizeof(N.Hit) + int(H.n_cigar) * 4},
         "index_build_s": round(t_build, 2),
     }
     if args.checksums:   # member k's rows with member-local read indices (= a one-GPU run with --seed-offset k)
@@ -479,7 +513,7 @@ def run_group(args, cfg) -> int:
         result["roofline"] = make_roofline(names[di], di, iso[0], iso[1], r0.n, iso, r0.n, per_read, tr, 1)
         result["kernels"] = {STAGE_KERNEL[names[i]]: {"lone_ms": round(iso[0][i], 3)} for i in range(4)}
     hb.stop()
-    print(json.dumps(result), flush=True)
+    print(json.dumps(result), file=json_out(), flush=True)
     L.bsq_group_free(g)
     L.bsq_index_free(idx)
     return 0
@@ -515,6 +549,9 @@ def main() -> int:
     ap.add_argument("--group-devices", default=None,
                     help="in-process group (--gpus N without torchrun): comma-separated device of each member "
                          "(default 0..N-1; a repeated device makes replicas on one GPU, for tests)")
+    ap.add_argument("--exchange", default="links", choices=["links", "via-first"],
+                    help="in-process group: records to host over every member's own link (links) or gathered over "
+                         "xGMI into member 0 first (via-first)")
     ap.add_argument("--lockstep", action="store_true",
                     help="a barrier after every timed step (bsq_batch_run_many per step) instead of one stream of "
                          "batch runs over the K steps")
@@ -528,6 +565,7 @@ def main() -> int:
     ap.add_argument("--checksums", action="store_true",
                     help="add the oracle-format checksum of every rank/member's full read set to the line")
     args = ap.parse_args()
+    json_out()
     if args.timed_only:
         args.no_cpu_baseline = args.no_codec = args.no_isolated = True
     if args.cursor_only:
@@ -660,13 +698,33 @@ def main() -> int:
                     parts.append(np.ctypeslib.as_array(ctypes.cast(H.cigar, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nc, 1),))[:nc])
                 xchg.post(parts)
 
-    xchg = None
-    if dist is not None:
+    xchg = None    # the Python exchange (gloo rehearsal only)
+    nx = None      # the native exchange: bsq_xchg lanes over RCCL, one per batch
+    if dist is not None and args.dist_backend == "nccl" and not cfg["seeding"]:
+        import torch
+        IDB = 128   # BSQ_XCHG_ID_BYTES
+        ids = torch.zeros(S * IDB, dtype=torch.uint8, device=xdev)
+        if rank == 0:
+            raw = ctypes.create_string_buffer(S * IDB)
+            for k in range(S):
+                N.check(L.bsq_xchg_unique_id(ctypes.addressof(raw) + k * IDB))
+            ids.copy_(torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8))
+        dist.broadcast(ids, src=0)
+        idb = ctypes.create_string_buffer(bytes(ids.cpu().numpy()), S * IDB)
+        nx = ctypes.c_void_p()
+        hb.phase = "joining the exchange lanes"
+        N.check(L.bsq_xchg_create(world, rank, gpu, idb, S, ctypes.byref(nx)))
+    elif dist is not None:
         from bioseqdb_amd import dist as D
         xchg = D.RecordExchange(device=xdev)
     hb.phase = "aligning"
-    for _ in range(args.warmup):
-        step()
+    moved0 = ctypes.c_int64()
+    if nx is not None:
+        N.check(L.bsq_batch_run_rounds_x(b_arr, S, ctypes.byref(opts), fc_arr, args.warmup, nx))
+        N.check(L.bsq_xchg_finish(nx, ctypes.byref(moved0), None))
+    else:
+        for _ in range(args.warmup):
+            step()
     if xchg is not None:
         xchg.finish()
     stage_ms = np.zeros(6)
@@ -680,13 +738,19 @@ def main() -> int:
     # its next step as soon as its previous one ends, so one batch's seeding overlaps the others' DP tails
     # instead of every step draining to a barrier; every step still aligns all the reads once, and the last
     # step's records are checked below.  --lockstep: a barrier after every step (bsq_batch_run_many per step).
-    rounds = dist is None and S > 1 and not cfg["seeding"] and not args.lockstep
+    # Under torchrun (RCCL) every rank runs the same stream of rounds, each batch's records going to rank 0 over its
+    # exchange lane after every round (bsq_batch_run_rounds_x).
+    rounds = (dist is None or nx is not None) and S > 1 and not cfg["seeding"] and not args.lockstep
     t0 = time.perf_counter()
     if rounds:
-        N.check(L.bsq_batch_run_rounds(b_arr, S, ctypes.byref(opts), fc_arr, args.steps))
+        N.check(L.bsq_batch_run_rounds_x(b_arr, S, ctypes.byref(opts), fc_arr, args.steps, nx))
     for _ in range(1 if rounds else args.steps):
         if not rounds:
-            step()
+            if nx is not None:
+                N.check(L.bsq_batch_run_rounds_x(b_arr, S, ctypes.byref(opts), fc_arr, 1, nx))
+                N.check(L.bsq_xchg_finish(nx, None, None))
+            else:
+                step()
         for b in batches:   # per-launch figures: averaged over the S concurrent launches of each stage
             ms = (ctypes.c_float * 6)()
             L.bsq_batch_stage_ms(b, ms, 6)
@@ -697,9 +761,13 @@ def main() -> int:
             stage_work += np.array(list(wk))
             stage_ms += np.array(list(ms))
             stage_bytes += np.array(list(by))
+    moved1, xwait = ctypes.c_int64(), ctypes.c_double()
     if dist is not None:
         import torch
-        xchg.finish()   # the last step's records are on the caller's host
+        if nx is not None:   # the last round's records of every rank are in rank 0's host memory
+            N.check(L.bsq_xchg_finish(nx, ctypes.byref(moved1), ctypes.byref(xwait)))
+        else:
+            xchg.finish()   # the last step's records are on the caller's host
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -758,11 +826,17 @@ def main() -> int:
             "step_schedule": ("stream of batch runs over the timed steps (bsq_batch_run_rounds; stage times of the "
                               "last step)" if rounds else "barrier after every step"),
         },
-        "exchange": None if xchg is None else {
-            "path": ("RCCL gather of device records to rank 0, pinned D2H there, overlapped with the next step"
-                     if xchg.gpu else "gloo gather of host records to rank 0 (rehearsal)"),
+        "exchange": ({
+            "path": ("bsq_xchg: per round and lane (= batch) an RCCL all-gather of the record counts, then every rank's "
+                     "read offsets, hits and CIGAR words ncclSend/ncclRecv to rank 0 over xGMI and its pinned D2H there; "
+                     "the batch's next round waits only for its own send"),
+            "lanes": S, "bytes_per_step": int((moved1.value - moved0.value) / max(args.steps, 1)),
+            "bytes_side": "received by rank 0" if rank == 0 else "sent by this rank",
+            "host_wait_ms_per_step_per_lane": round(xwait.value / max(args.steps, 1) / S, 3),
+        } if nx is not None else None if xchg is None else {
+            "path": "gloo gather of host records to rank 0 (rehearsal)",
             "bytes_per_step_rank0": int(xchg.bytes_moved / max(args.steps + args.warmup, 1)) if rank == 0 else None,
-        },
+        }),
         "kernels": {
             STAGE_KERNEL[nm]: {
                 "ms": round(float(stage_ms[i]), 3), "issued_bytes": float(stage_bytes[i]),
@@ -787,6 +861,31 @@ def main() -> int:
         for k, b in enumerate(batches):
             ck += gpu_checksum_vec(L.bsq_batch_hits(b).contents, lo_k[k + 1] - lo_k[k], lo_k[k])
         result["checksums"] = [ck & 0xFFFFFFFFFFFFFFFF]
+        if nx is not None and rank == 0:   # every other rank's records as rank 0 received them (= a one-GPU run
+            for r in range(1, world):      # with --seed-offset r)
+                ck = 0
+                for k in range(S):
+                    v = N.Hits()
+                    N.check(L.bsq_xchg_view(nx, k, r, ctypes.byref(v)))
+                    ck += gpu_checksum_vec(v, lo_k[k + 1] - lo_k[k], lo_k[k])
+                result["checksums"].append(ck & 0xFFFFFFFFFFFFFFFF)
+
+    # ---- N > 1: the last rank's records as rank 0 received them, against the CPU oracle on a sample ----
+    if nx is not None and world > 1 and rank == 0 and not args.no_cpu_baseline:
+        hb.phase = "oracle parity sample of the exchanged records"
+        r_last = world - 1
+        rr = synth.make_reads(ref, args.reads, length=args.read_len, seed=synth.READ_SEED + r_last + args.seed_offset)
+        m = min(2000, lo_k[1])
+        O, oi = oracle_index(L, idx, ref_ns)
+        oo = O.opts_from(opts)
+        c_, o_ = np.ascontiguousarray(rr.codes), np.ascontiguousarray(rr.offsets)
+        ck = ctypes.c_uint64()
+        O.lib().orc_align_batch(oi.h, ctypes.byref(oo), c_.ctypes.data, o_.ctypes.data, m,
+                                (r_last + args.seed_offset) * args.reads, host_cpus()["usable"], ctypes.byref(ck))
+        v = N.Hits()
+        N.check(L.bsq_xchg_view(nx, 0, r_last, ctypes.byref(v)))
+        result["parity_sample"] = {"rank": r_last, "reads": m, "received_by_rank0": True,
+                                   "checksum_match": (gpu_checksum_vec(v, m, 0) & 0xFFFFFFFFFFFFFFFF) == ck.value}
 
     # ---- host materialisation: the last step's rows rendered as bwa_result text ----
     if rank == 0 and not cfg["seeding"] and n_hits and not args.timed_only:
@@ -1027,7 +1126,9 @@ def main() -> int:
     result["roofline"] = make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, reads.n, per_read, tr, S)
     hb.stop()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out(), flush=True)
+    if nx is not None:
+        L.bsq_xchg_free(nx)
     for b in batches:
         L.bsq_batch_free(b)
     L.bsq_index_free(idx)

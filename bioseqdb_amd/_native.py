@@ -135,6 +135,16 @@ SIGNATURES = {
     "bsq_group_hits": (ctypes.POINTER(Hits), [_P]),
     "bsq_group_render_nuclseqs": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "bsq_group_set_slots": (ctypes.c_int, [_P, ctypes.c_int]),
+    "bsq_group_run_rounds": (ctypes.c_int, [_P, ctypes.POINTER(Opts), ctypes.c_int32, ctypes.c_uint64, ctypes.c_int]),
+    "bsq_group_set_exchange": (ctypes.c_int, [_P, ctypes.c_int]),
+    "bsq_batch_set_record_route": (ctypes.c_int, [_P, ctypes.c_int]),
+    "bsq_xchg_unique_id": (ctypes.c_int, [_P]),
+    "bsq_xchg_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.POINTER(_P)]),
+    "bsq_xchg_free": (None, [_P]),
+    "bsq_batch_run_rounds_x": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(Opts),
+                                              ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _P]),
+    "bsq_xchg_finish": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "bsq_xchg_view": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Hits)]),
     "bsq_group_segments": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(Hits)), ctypes.POINTER(ctypes.c_int32),
                                           ctypes.c_int]),
     "bsq_pipeline_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P)]),

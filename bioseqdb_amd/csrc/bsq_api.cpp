@@ -897,6 +897,14 @@ struct bsq_batch {
     double stage_work[STG_N]{};
     int64_t retried = 0;
     bool dev_whole = false;   // d_out / d_out_cig hold the whole last run's view (one chunk, no retried read)
+    // record route (bsq_batch_set_record_route): the packed records cross to relay_dev's HBM by peer DMA (xGMI between
+    // devices) and reach the pinned view over that device's PCIe link instead of this device's own
+    int relay_dev = -1;
+    uint8_t *relay = nullptr;
+    int64_t relay_cap = 0;
+    hipStream_t relay_stream = nullptr;   // on relay_dev
+    hipEvent_t relay_in = nullptr;        // on this device: the records are packed
+    hipEvent_t relay_out = nullptr;       // on relay_dev: they are in host memory
 };
 
 static const char *kStageNames[STG_N] = {"smem", "chain", "extend", "reg2aln", "pack", "d2h"};
@@ -998,6 +1006,14 @@ extern "C" void bsq_batch_free(bsq_batch *b)
     hipFree(b->r_qh); hipFree(b->r_qoff); hipHostFree(b->c_host); hipHostFree(b->c_off);
     hipFree(b->ns_dev); hipFree(b->ns_meta);
     for (auto &e : b->ev) if (e) hipEventDestroy(e);
+    if (b->relay_in) hipEventDestroy(b->relay_in);
+    if (b->relay_dev >= 0) {
+        hipSetDevice(b->relay_dev);
+        if (b->relay_stream) { hipStreamSynchronize(b->relay_stream); hipStreamDestroy(b->relay_stream); }
+        if (b->relay_out) hipEventDestroy(b->relay_out);
+        hipFree(b->relay);
+        hipSetDevice(b->device);
+    }
     if (b->stream) hipStreamDestroy(b->stream);
     if (b->cstream && b->cstream != b->stream) { hipStreamSynchronize(b->cstream); hipStreamDestroy(b->cstream); }
     delete b;
@@ -1327,6 +1343,86 @@ static int grow_pinned(T *&p, int64_t &cap, int64_t need, int64_t keep)
     return BSQ_OK;
 }
 
+// The relayed record route: read offsets, hits and CIGARs of the packed chunk by peer DMA into relay_dev's HBM
+// (one buffer, 256-B aligned parts), then D2H from there on relay_dev's stream into the same pinned arrays the
+// direct route fills; the batch stream waits for the D2H, so the stage events and the view are unchanged.
+static int relay_records(bsq_batch *b, int n, int lo, int64_t hit_dst, int64_t cig_dst, const int64_t tot[2])
+{
+    hipStream_t st = b->stream;
+    auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    const int64_t o_off = 0, o_hit = al((int64_t)(n + 1) * 8), o_cig = o_hit + al(tot[0] * (int64_t)sizeof(bsq_hit));
+    const int64_t need = o_cig + al(tot[1] * 4);
+    if (need > b->relay_cap) {
+        HIPCHK(hipSetDevice(b->relay_dev));
+        hipStreamSynchronize(b->relay_stream);
+        hipFree(b->relay);
+        b->relay = nullptr;
+        b->relay_cap = 0;
+        const int64_t cap = std::max<int64_t>(need + need / 4, 1 << 20);
+        const hipError_t e = hipMalloc(&b->relay, (size_t)cap);
+        hipSetDevice(b->device);
+        if (e != hipSuccess) { set_err("relay buffer on device %d: %s", b->relay_dev, hipGetErrorString(e)); return BSQ_E_NOMEM; }
+        b->relay_cap = cap;
+    }
+    uint8_t *r = b->relay;
+    HIPCHK(hipMemcpyPeerAsync(r + o_off, b->relay_dev, b->off_hits, b->device, (size_t)(n + 1) * 8, st));
+    if (tot[0]) HIPCHK(hipMemcpyPeerAsync(r + o_hit, b->relay_dev, b->d_out, b->device, (size_t)tot[0] * sizeof(bsq_hit), st));
+    if (tot[1]) HIPCHK(hipMemcpyPeerAsync(r + o_cig, b->relay_dev, b->d_out_cig, b->device, (size_t)tot[1] * 4, st));
+    HIPCHK(hipEventRecord(b->relay_in, st));
+    HIPCHK(hipSetDevice(b->relay_dev));
+    hipStream_t rs = b->relay_stream;
+    hipError_t e = hipStreamWaitEvent(rs, b->relay_in, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(b->h_pinned_off + lo, r + o_off, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, rs);
+    if (e == hipSuccess && tot[0])
+        e = hipMemcpyAsync(b->h_pinned + hit_dst, r + o_hit, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, rs);
+    if (e == hipSuccess && tot[1])
+        e = hipMemcpyAsync(b->h_pinned_cig + cig_dst, r + o_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, rs);
+    if (e == hipSuccess) e = hipEventRecord(b->relay_out, rs);
+    hipSetDevice(b->device);
+    if (e != hipSuccess) { set_err("record relay: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
+    HIPCHK(hipStreamWaitEvent(st, b->relay_out, 0));
+    return BSQ_OK;
+}
+
+extern "C" int bsq_batch_set_record_route(bsq_batch *b, int via_device)
+{
+    if (!b || via_device < -1) { set_err("invalid argument"); return BSQ_E_INVALID; }
+    if (via_device == b->relay_dev) return BSQ_OK;
+    int ndev = 0;
+    if (via_device >= 0 && (hipGetDeviceCount(&ndev) != hipSuccess || via_device >= ndev)) {
+        set_err("no HIP device %d", via_device);
+        return BSQ_E_NODEV;
+    }
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    if (b->relay_dev >= 0) {   // drop the previous route's buffers
+        hipSetDevice(b->relay_dev);
+        hipStreamSynchronize(b->relay_stream);
+        hipStreamDestroy(b->relay_stream);
+        hipEventDestroy(b->relay_out);
+        hipFree(b->relay);
+        hipSetDevice(b->device);
+        hipEventDestroy(b->relay_in);
+        b->relay_stream = nullptr; b->relay_out = nullptr; b->relay = nullptr; b->relay_in = nullptr;
+        b->relay_cap = 0;
+        b->relay_dev = -1;
+    }
+    if (via_device < 0) return BSQ_OK;
+    if (via_device != b->device) {   // peer DMA over xGMI (already enabled is fine)
+        const hipError_t e = hipDeviceEnablePeerAccess(via_device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { set_err("peer access %d -> %d: %s", b->device, via_device, hipGetErrorString(e)); return BSQ_E_HIP; }
+        (void)hipGetLastError();
+    }
+    HIPCHK(hipEventCreateWithFlags(&b->relay_in, hipEventDisableTiming));
+    HIPCHK(hipSetDevice(via_device));
+    hipError_t e = hipStreamCreateWithFlags(&b->relay_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b->relay_out, hipEventDisableTiming);
+    hipSetDevice(b->device);
+    if (e != hipSuccess) { set_err("relay stream: %s", hipGetErrorString(e)); return BSQ_E_HIP; }
+    b->relay_dev = via_device;
+    return BSQ_OK;
+}
+
 // Main-pass chunk [lo, lo + n): records land in the batch-wide pinned arrays at hit_dst / cig_dst with
 // batch-wide read indices and CIGAR offsets, read_off[lo .. lo + n] = batch-wide hit offsets.
 static int pack_main(bsq_batch *b, Workspace &w, int n, int lo, int64_t hit_dst, int64_t cig_dst, int64_t tot[2])
@@ -1339,9 +1435,14 @@ static int pack_main(bsq_batch *b, Workspace &w, int n, int lo, int64_t hit_dst,
     { int rc = grow_pinned(b->h_pinned_off, b->h_off_cap, (int64_t)b->n_reads + 1, lo); if (rc) return rc; }
     HIPCHK(launch_add_base(st, b->off_hits, n + 1, hit_dst));
     HIPCHK(hipEventRecord(b->ev[STG_D2H], st));
-    HIPCHK(hipMemcpyAsync(b->h_pinned_off + lo, b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
-    if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned + hit_dst, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
-    if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig + cig_dst, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
+    if (b->relay_dev >= 0) {
+        const int rc = relay_records(b, n, lo, hit_dst, cig_dst, tot);
+        if (rc) return rc;
+    } else {
+        HIPCHK(hipMemcpyAsync(b->h_pinned_off + lo, b->off_hits, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, st));
+        if (tot[0]) HIPCHK(hipMemcpyAsync(b->h_pinned + hit_dst, b->d_out, (size_t)tot[0] * sizeof(bsq_hit), hipMemcpyDeviceToHost, st));
+        if (tot[1]) HIPCHK(hipMemcpyAsync(b->h_pinned_cig + cig_dst, b->d_out_cig, (size_t)tot[1] * 4, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(hipEventRecord(b->ev[STG_N], st));
     HIPCHK(hipStreamSynchronize(st));
     return BSQ_OK;
@@ -1753,6 +1854,22 @@ extern "C" int bsq_batch_copy_records(const bsq_batch *b, void *dst, int64_t cap
 }
 
 extern "C" const bsq_hits *bsq_batch_hits(const bsq_batch *b) { return b ? &b->view : nullptr; }
+
+namespace bsq {
+BatchRecords batch_records(const bsq_batch *b)
+{
+    BatchRecords r;
+    r.device = b->device;
+    r.stream = b->stream;
+    r.on_device = b->dev_whole;
+    r.n_reads = b->view.n_reads;
+    r.n_hits = b->view.n_hits;
+    r.n_cigar = b->view.n_cigar;
+    if (b->dev_whole) { r.off = b->off_hits; r.hits = b->d_out; r.cig = b->d_out_cig; }
+    else { r.off = b->view.read_off; r.hits = b->view.hits; r.cig = b->view.cigar; }
+    return r;
+}
+}  // namespace bsq
 
 // Several batches in flight at once, one host thread and one stream each: the stages of one batch fill
 // the tails and host gaps of the others (3 batches of 1/3 of the reads: +24 % reads/s at C3 on one

@@ -36,6 +36,21 @@ int32_t batch_max_reads(const bsq_batch *b);
 int64_t batch_max_bases(const bsq_batch *b);
 
 void set_error(const std::string &msg);
+
+// Where the last bsq_batch_run's records are (exchange.cpp's send side): on the device when the packed arrays hold
+// the whole view (one workspace chunk, no retried read: off = batch-wide read offsets, hits, cig in HBM), else
+// the pinned host view.  `stream` is the batch's stream (the next run on it overwrites these arrays).
+struct BatchRecords {
+    int device = 0;
+    void *stream = nullptr;   // hipStream_t
+    bool on_device = false;
+    const int64_t *off = nullptr;
+    const bsq_hit *hits = nullptr;
+    const uint32_t *cig = nullptr;
+    int32_t n_reads = 0;
+    int64_t n_hits = 0, n_cigar = 0;
+};
+BatchRecords batch_records(const bsq_batch *b);
 // bsq_batch_render_nuclseqs into the batch's own pinned buffers: *out / *out_off are borrowed until the next
 // render or run of the batch (the pipeline hands them out until the slot is released).
 int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **out, const int64_t **out_off);
@@ -50,6 +65,9 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
 // With nothing outstanding, the next submission goes to slot 0 again (a caller that submits shares j = 0..s-1 per
 // round keeps share j on slot j, where a RERUN finds its staging).  BSQ_E_INVALID while submissions are pending.
 int pipeline_rewind(bsq_pipeline *p);
+// Record route of every batch of the pipeline (bsq_batch_set_record_route; -1: each batch's own device link).
+// BSQ_E_INVALID while submissions are pending.
+int pipeline_set_record_route(bsq_pipeline *p, int via_device);
 // bsq_pipeline_next plus the batch that holds the taken submission's records (NULL for an empty one)
 int pipeline_next_ex(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off,
                      bsq_batch **batch);

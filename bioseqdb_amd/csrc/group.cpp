@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -41,6 +42,7 @@ using bsq::PipeMode;
 using bsq::pipeline_next_ex;
 using bsq::pipeline_submit_ex;
 using bsq::pipeline_rewind;
+using bsq::pipeline_set_record_route;
 
 namespace {
 
@@ -72,6 +74,7 @@ struct bsq_group {
     bool rccl = false;                   // distinct devices: RCCL communicators; a repeated device: D2D copies
     bsq_index *src = nullptr;
     int slots = 4;                       // concurrent shares per member (bsq_group_set_slots)
+    int exchange = BSQ_XCHG_LINKS;       // how the records reach the host (bsq_group_set_exchange)
     int32_t n_reads = 0;
     bool merged = false;                 // hits/cigar/read_off hold the last run's segments
     std::vector<bsq_hit> hits;
@@ -150,6 +153,7 @@ extern "C" int bsq_group_create(const int *devices, int n_devices, bsq_group **o
     std::vector<int> sorted = dl;
     std::sort(sorted.begin(), sorted.end());
     g->rccl = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (const char *e = getenv("BSQ_GROUP_RCCL")) g->rccl = g->rccl && atoi(e) != 0;   // 0: peer copies only
     for (int k = 0; k < n_devices; ++k) {
         Member &x = g->m[(size_t)k];
         x.device = dl[(size_t)k];
@@ -257,8 +261,25 @@ extern "C" int bsq_group_replicate(bsq_group *g, bsq_index *idx, double *broadca
         if (rc) { const std::string m = bsq_last_error(); drop_replicas(g); return fail(rc, m); }
     }
     for (size_t k = 0; k < G; ++k) {
-        const int rc = bsq_pipeline_create(g->m[k].index, g->slots, &g->m[k].pipe);
+        int rc = bsq_pipeline_create(g->m[k].index, g->slots, &g->m[k].pipe);
+        if (!rc) rc = pipeline_set_record_route(g->m[k].pipe, g->exchange == BSQ_XCHG_VIA_FIRST && k > 0 ? dev0 : -1);
         if (rc) { const std::string m = bsq_last_error(); drop_replicas(g); return fail(rc, m); }
+    }
+    return BSQ_OK;
+}
+
+extern "C" int bsq_group_set_exchange(bsq_group *g, int mode)
+{
+    if (!g || (mode != BSQ_XCHG_LINKS && mode != BSQ_XCHG_VIA_FIRST)) return fail(BSQ_E_INVALID, "invalid argument");
+    g->merged = false;
+    g->view = bsq_hits{};
+    for (Member &x : g->m) release_held(x);   // the held views' slots must be free to re-route
+    g->exchange = mode;
+    for (Member &x : g->m) {
+        if (!x.pipe) continue;   // not replicated yet: applied at bsq_group_replicate
+        // member 0's records take its own link either way (the relay would copy them onto the same device)
+        const int rc = pipeline_set_record_route(x.pipe, mode == BSQ_XCHG_VIA_FIRST && &x != &g->m[0] ? g->m[0].device : -1);
+        if (rc) return rc;
     }
     return BSQ_OK;
 }
@@ -269,6 +290,39 @@ extern "C" int bsq_group_set_slots(bsq_group *g, int slots)
     if (g->src) return fail(BSQ_E_INVALID, "set the slots before bsq_group_replicate");
     g->slots = slots;
     return BSQ_OK;
+}
+
+static int finish_run(bsq_group *g, int rc);
+
+// One round of a member's shard: share j submitted to slot j (staged from `reads`, or re-run from the slot's
+// staging when reads == NULL), then every share taken in order and held.
+static int member_round(Member &x, const bsq_opts *opts, const void *const *reads, uint64_t first_call_seq)
+{
+    if (x.n == 0) return BSQ_OK;
+    const int s = (int)x.slo.size() - 1;
+    int rc = pipeline_rewind(x.pipe), submitted = 0;   // share j on slot j (a re-run finds its staging there)
+    for (int j = 0; j < s && rc == BSQ_OK; ++j) {
+        const int32_t a = x.lo + x.slo[(size_t)j], n = x.slo[(size_t)j + 1] - x.slo[(size_t)j];
+        rc = reads ? pipeline_submit_ex(x.pipe, opts, reads + a, n, first_call_seq + (uint64_t)a, 0, PipeMode::DEFER)
+                   : pipeline_submit_ex(x.pipe, opts, nullptr, n, first_call_seq + (uint64_t)a, 0, PipeMode::RERUN);
+        if (rc == BSQ_OK) ++submitted;
+    }
+    std::string err;
+    for (int j = 0; j < submitted; ++j) {   // every submission is taken, failed or not
+        const bsq_hits *v = nullptr;
+        bsq_batch *b = nullptr;
+        const int r = pipeline_next_ex(x.pipe, &v, nullptr, nullptr, &b);
+        if (r) { if (rc == BSQ_OK) { rc = r; err = bsq_last_error(); } continue; }
+        x.views.push_back(v);
+        x.batches.push_back(b);
+    }
+    if (rc != BSQ_OK) {
+        if (!err.empty()) bsq_internal_set_error(err.c_str());
+        const std::string m = bsq_last_error();
+        release_held(x);
+        bsq_internal_set_error(m.c_str());
+    }
+    return rc;
 }
 
 extern "C" int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
@@ -295,34 +349,43 @@ extern "C" int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *con
             for (int j = 0; j <= s; ++j) x.slo[(size_t)j] = (int32_t)((int64_t)x.n * j / s);
         }
     } else if (n_reads != g->n_reads) return fail(BSQ_E_INVALID, "re-run of a different read count");
+    const int rc = for_members(g, [&](int k) -> int { return member_round(g->m[(size_t)k], opts, reads, first_call_seq); });
+    return finish_run(g, rc);
+}
+
+extern "C" int bsq_group_run_rounds(bsq_group *g, const bsq_opts *opts, int32_t n_reads, uint64_t first_call_seq, int rounds)
+{
+    if (!g || !opts || rounds < 1) return fail(BSQ_E_INVALID, "invalid argument");
+    if (!g->src) return fail(BSQ_E_INVALID, "no index replicated on the group (bsq_group_replicate)");
+    if (n_reads != g->n_reads) return fail(BSQ_E_INVALID, "re-run of a different read count");
+    g->merged = false;
+    g->view = bsq_hits{};
     const int rc = for_members(g, [&](int k) -> int {
         Member &x = g->m[(size_t)k];
-        if (x.n == 0) return BSQ_OK;
         const int s = (int)x.slo.size() - 1;
-        int rc = pipeline_rewind(x.pipe), submitted = 0;   // share j on slot j (a re-run finds its staging there)
-        for (int j = 0; j < s && rc == BSQ_OK; ++j) {
-            const int32_t a = x.lo + x.slo[(size_t)j], n = x.slo[(size_t)j + 1] - x.slo[(size_t)j];
-            rc = reads ? pipeline_submit_ex(x.pipe, opts, reads + a, n, first_call_seq + (uint64_t)a, 0, PipeMode::DEFER)
-                       : pipeline_submit_ex(x.pipe, opts, nullptr, n, first_call_seq + (uint64_t)a, 0, PipeMode::RERUN);
-            if (rc == BSQ_OK) ++submitted;
-        }
-        std::string err;
-        for (int j = 0; j < submitted; ++j) {   // every submission is taken, failed or not
-            const bsq_hits *v = nullptr;
-            bsq_batch *b = nullptr;
-            const int r = pipeline_next_ex(x.pipe, &v, nullptr, nullptr, &b);
-            if (r) { if (rc == BSQ_OK) { rc = r; err = bsq_last_error(); } continue; }
-            x.views.push_back(v);
-            x.batches.push_back(b);
-        }
-        if (rc != BSQ_OK) {
-            if (!err.empty()) bsq_internal_set_error(err.c_str());
-            const std::string m = bsq_last_error();
+        if (x.n == 0 || s < 1) return BSQ_OK;
+        int todo = rounds;
+        bool held = (int)x.batches.size() == s;
+        for (bsq_batch *b : x.batches) held = held && b;
+        if (!held) {   // the previous run's shares are not all held on their batches: one staged round first
             release_held(x);
-            bsq_internal_set_error(m.c_str());
+            const int r = member_round(x, opts, nullptr, first_call_seq);
+            if (r || --todo == 0) return r;
         }
-        return rc;
+        // The shares' batches (held since the last run, reads resident) run bsq_batch_run_rounds' schedule: each
+        // share's thread starts its next round as soon as its last one ends, so the shares drift out of phase and
+        // one's seeding overlaps the others' DP stages (the pipeline's in-order turns would keep them in step).
+        std::vector<uint64_t> fc((size_t)s);
+        for (int j = 0; j < s; ++j) fc[(size_t)j] = first_call_seq + (uint64_t)(x.lo + x.slo[(size_t)j]);
+        const int r = bsq_batch_run_rounds(x.batches.data(), s, opts, fc.data(), todo);
+        if (r) release_held(x);
+        return r;
     });
+    return finish_run(g, rc);
+}
+
+static int finish_run(bsq_group *g, int rc)
+{
     if (rc) {
         for (Member &x : g->m) release_held(x);
         return rc;

@@ -84,6 +84,7 @@ struct bsq_pipeline {
     uint64_t n_submit = 0, n_take = 0, n_release = 0;   // slot of job j is s[j % S]
     uint64_t run_started = 0;                           // jobs whose alignment turn has begun
     int running = 0, run_cap = 4;                       // alignments on the device now, and at most
+    int route_via = -1;                                 // record route of the slots' batches (group exchange)
     std::vector<std::array<double, 7>> trace;           // BSQ_PIPE_TRACE: per job, slot then Slot::t
     std::mutex mu;
     std::condition_variable cv;
@@ -125,6 +126,7 @@ int prep_job(bsq_pipeline *p, Slot &x)
         x.cap_reads = std::max(r, 1);
         x.cap_bases = std::max<int64_t>(b, 1);
     }
+    { const int rc = bsq_batch_set_record_route(x.batch, p->route_via); if (rc) return rc; }   // no-op when unchanged
     if (!x.resident) {
         const int rc = batch_upload_staged(x.batch, x.stage);
         if (rc) return rc;
@@ -259,6 +261,14 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
     x->state = SlotState::QUEUED;
     ++p->n_submit;
     p->cv.notify_all();
+    return BSQ_OK;
+}
+
+int pipeline_set_record_route(bsq_pipeline *p, int via_device)
+{
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->n_release != p->n_submit) return fail(BSQ_E_INVALID, "pipeline has outstanding submissions");
+    p->route_via = via_device;   // applied by each slot's worker before its next alignment
     return BSQ_OK;
 }
 

@@ -189,6 +189,19 @@ int bsq_group_run(bsq_group *g, const bsq_opts *opts, const void *const *reads, 
 /* Concurrent shares per member (1..16, default 4): each member splits its shard into up to this many batches
  * of >= 32768 reads that run at once on its device (a bsq_pipeline).  Set before bsq_group_replicate. */
 int bsq_group_set_slots(bsq_group *g, int slots);
+/* bsq_group_run `rounds` times over the reads staged by the previous bsq_group_run (n_reads as given there), with
+ * no barrier between rounds: each member's shares run bsq_batch_run_rounds on the batches that hold them (share j
+ * starts its next round as soon as its previous one ends), the schedule of the one-device bench.  Every round
+ * aligns every read from first_call_seq; the last round's records are the result (segments / merged view as after
+ * bsq_group_run). */
+int bsq_group_run_rounds(bsq_group *g, const bsq_opts *opts, int32_t n_reads, uint64_t first_call_seq, int rounds);
+/* How the members' records reach host memory (the exchange step of a sharded call):
+ * BSQ_XCHG_LINKS     each member's records over its own PCIe link (default; all links at once);
+ * BSQ_XCHG_VIA_FIRST each member's records by peer DMA over xGMI into member 0's HBM, then over member 0's link
+ *                    (the records gathered on one device first).  Set between runs. */
+#define BSQ_XCHG_LINKS 0
+#define BSQ_XCHG_VIA_FIRST 1
+int bsq_group_set_exchange(bsq_group *g, int mode);
 /* The merged view of the last run (built on first call after a run; NULL on allocation failure). */
 const bsq_hits *bsq_group_hits(const bsq_group *g);
 /* The last run's records without the merge: segment i (one per member share, in read order) covers reads
@@ -198,6 +211,30 @@ int bsq_group_segments(const bsq_group *g, const bsq_hits **views, int32_t *read
 /* build_tuple_bwa's two nuclseq columns of the last run's rows, rendered on every member for its shard
  * (layout as bsq_batch_render_nuclseqs, rows in the merged order).  `reads` as given to bsq_group_run. */
 int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads, uint8_t **out, int64_t **out_off);
+
+/* ---- One process per GPU (torchrun): the record exchange to rank 0 ----
+ * Every rank's hit records return to the caller (rank 0), the rows nuclseq_multi_search_bwa puts into its
+ * tuplestore (extension.cpp:362-370).  Lane i (one RCCL communicator + stream) carries batch i of every rank:
+ * after each round the lane all-gathers the ranks' record counts, every rank r > 0 sends its read offsets, hits
+ * and CIGAR words to rank 0 (ncclSend/ncclRecv over xGMI) and rank 0 copies them to pinned host memory. */
+typedef struct bsq_xchg bsq_xchg;
+#define BSQ_XCHG_ID_BYTES 128
+/* A fresh communicator id (BSQ_XCHG_ID_BYTES bytes) -- rank 0 makes one per lane and the launcher's own channel
+ * (torch.distributed) hands them to every rank. */
+int bsq_xchg_unique_id(void *id);
+/* Joins the `lanes` communicators (ids: lanes x BSQ_XCHG_ID_BYTES, the same on every rank) on `device`; collective. */
+int bsq_xchg_create(int world, int rank, int device, const void *ids, int lanes, bsq_xchg **out);
+void bsq_xchg_free(bsq_xchg *x);
+/* bsq_batch_run_rounds with lane i exchanging batch i's records after every round (n == lanes on every rank);
+ * x == NULL: bsq_batch_run_rounds. */
+int bsq_batch_run_rounds_x(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call,
+                           int rounds, bsq_xchg *x);
+/* Waits for every lane's last exchange (rank 0: the records are in its host memory).  *bytes_moved: bytes
+ * received (rank 0) or sent (others) over all rounds; *wait_ms: host time the batch threads spent exchanging. */
+int bsq_xchg_finish(bsq_xchg *x, int64_t *bytes_moved, double *wait_ms);
+/* Rank 0: the last round's records of lane `lane` from rank src_rank > 0 (read_index and cigar_off local to that
+ * rank's batch), borrowed until the next round or free. */
+int bsq_xchg_view(const bsq_xchg *x, int lane, int src_rank, bsq_hits *out);
 
 /* ---- Pipelined cursor fetches (replaces the fetch-align-materialise loop of
  * nuclseq_multi_search_bwa, extension.cpp:156-195 + 362-370, which leaves the device idle between fetches).
@@ -286,6 +323,10 @@ int bsq_batch_run_many(bsq_batch *const *batches, int n, const bsq_opts *opts, c
  * round's. */
 int bsq_batch_run_rounds(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call,
                          int rounds);
+/* Where bsq_batch_run copies the packed records: via_device = -1 (default) over this device's PCIe link into the
+ * pinned view; via_device >= 0: by peer DMA (xGMI) into that device's HBM and from there into the same pinned view
+ * over its link (the gather-to-one-device exchange of a device group).  The view and stage times are unchanged. */
+int bsq_batch_set_record_route(bsq_batch *b, int via_device);
 /* Borrowed view of the last run's hits (valid until the next run or free). */
 const bsq_hits *bsq_batch_hits(const bsq_batch *b);
 /* The last run's records as bytes in device memory on the batch's device: the bsq_hit array, then the CIGAR

@@ -9,7 +9,10 @@ verified) from the GPU-built suffix array, which is unique, so nothing else the 
 * all 14 bwa_result columns of 20k reads (bsq_align_batch + bsq_render_tsv, the path of
   BwaIndex::align_sequence, bwa.cpp:141-181) against the oracle's rows;
 * a second cursor batch that continues the backend's lrand48 stream (Q10);
-* bsq_batch_seed intervals (mem_collect_intv) of 20k reads on the same index.
+* bsq_batch_seed intervals (mem_collect_intv) of 20k reads on the same index;
+* the index replicated to a 2-member device group (SURVEY.md 8(e), C5's code path on one GPU: a repeated device
+  holds a replica imported from device-to-device copies of the 64-bit tables), 12k reads per member aligned with
+  the lrand48 stream continuing from an earlier call, every column against the oracle.
 The reference rows go through the GPU bulk codec (nuclseq_in, tested byte-for-byte in test_gpu_codec.py).
 """
 import ctypes
@@ -21,7 +24,7 @@ import pytest
 import oracle_py as O
 from bioseqdb_amd import BwaIndex, NucleotideSequence, effective_opts, loader, synth
 from bioseqdb_amd import _native as N
-from parity_util import compare_batch
+from parity_util import _oracle_batch_tsv, compare_batch, compare_tsv
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -107,3 +110,34 @@ def test_c4_3gbp_seeding(c4_pair):
             bad.append((r, got[:3], exp[:3]))
     assert total > 20_000
     assert not bad, bad[:5]
+
+
+def test_c4_3gbp_replicated_group(c4_pair):
+    ref, pi, oi = c4_pair
+    reads = synth.make_reads(ref, 24_000, seed=synth.READ_SEED + 3)
+    seqs = _seqs(reads)
+    n = len(seqs)
+    ptrs = (ctypes.c_void_p * n)(*[s.ptr for s in seqs])
+    L = N.lib()
+    g = ctypes.c_void_p()
+    N.check(L.bsq_group_create((ctypes.c_int * 2)(0, 0), 2, ctypes.byref(g)))
+    try:
+        N.check(L.bsq_group_set_exchange(g, 1))   # member 1's records through member 0's HBM
+        N.check(L.bsq_group_replicate(g, pi.handle, None))
+        first_call = 25_000   # continues the backend's lrand48 stream (Q10)
+        N.check(L.bsq_group_run(g, ctypes.byref(pi.options), ptrs, n, first_call))
+        N.check(L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n, first_call, 2))
+        H = L.bsq_group_hits(g)
+        segs = (ctypes.POINTER(N.Hits) * 16)()
+        slo = (ctypes.c_int32 * 16)()
+        assert L.bsq_group_segments(g, segs, slo, 16) == 2 and list(slo[:2]) == [0, n // 2]
+        p = L.bsq_render_tsv(pi.handle, H, ptrs)
+        text = ctypes.string_at(p).decode("latin-1")
+        L.bsq_free(p)
+        counts = [H.contents.read_off[i + 1] - H.contents.read_off[i] for i in range(n)]
+    finally:
+        L.bsq_group_free(g)
+    exp, ec = _oracle_batch_tsv(oi, O.opts_from(pi.options), [s.raw for s in seqs], first_call)
+    rows, bad = compare_tsv(text, counts, exp, ec)
+    assert rows > 22_000
+    assert not bad, bad[:20]

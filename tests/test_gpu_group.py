@@ -82,6 +82,36 @@ def test_group_rows_equal_one_device(setup, devices):
         L.bsq_group_free(g)
 
 
+
+@pytest.mark.parametrize("devices,slots,exchange", [([0], 1, 0), ([0, 0], 1, 1), ([0, 0, 0], 4, 1), ([0, 0], 4, 0)])
+def test_group_rounds_and_exchange_routes(setup, devices, slots, exchange):
+    """bsq_group_run_rounds (the bench's barrier-free stream of rounds: one share per slot streams, fewer shares
+    than slots run whole rounds) and the gather-to-member-0 exchange (BSQ_XCHG_VIA_FIRST: records by peer DMA into
+    member 0's HBM, then its link) give the rows of one device aligning all reads."""
+    pi, _, seqs = setup
+    L = N.lib()
+    n = len(seqs)
+    ptrs = (ctypes.c_void_p * n)(*[s.ptr for s in seqs])
+    want = _one_device(L, pi.handle, pi.options, ptrs, n, 99)
+    g = ctypes.c_void_p()
+    N.check(L.bsq_group_create((ctypes.c_int * len(devices))(*devices), len(devices), ctypes.byref(g)))
+    try:
+        N.check(L.bsq_group_set_slots(g, slots))
+        N.check(L.bsq_group_set_exchange(g, exchange))
+        N.check(L.bsq_group_replicate(g, pi.handle, None))
+        N.check(L.bsq_group_run(g, ctypes.byref(pi.options), ptrs, n, 99))
+        assert _records(L.bsq_group_hits(g).contents, n) == want
+        for rounds in (1, 3):
+            N.check(L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n, 99, rounds))
+            assert _records(L.bsq_group_hits(g).contents, n) == want, rounds
+        N.check(L.bsq_group_set_exchange(g, 1 - exchange))   # switched between runs
+        N.check(L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n, 99, 2))
+        assert _records(L.bsq_group_hits(g).contents, n) == want
+        assert L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n + 1, 99, 2) == N.BSQ_E_INVALID
+        assert L.bsq_group_set_exchange(g, 7) == N.BSQ_E_INVALID
+    finally:
+        L.bsq_group_free(g)
+
 def test_group_nuclseq_columns(setup):
     """build_tuple_bwa's two nuclseq columns rendered per member equal one batch's."""
     pi, _, seqs = setup

@@ -46,3 +46,39 @@ def test_group_bench_fails_loudly_without_enough_devices():
                        text=True, timeout=300, cwd=ROOT)
     assert r.returncode != 0
     assert "HIP device(s) visible" in r.stderr
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_group_bench_gather_via_first_member():
+    """--exchange via-first: member 1's records reach the host through member 0's HBM (peer DMA, then member 0's
+    link) under the stream-of-rounds schedule; the rows are the same as one-GPU runs'."""
+    g = _bench("--gpus", "2", "--group-devices", "0,0", "--exchange", "via-first", "--no-isolated")
+    assert g["exchange"]["mode"] == "via-first" and "xGMI" in g["exchange"]["path"]
+    assert "stream of rounds" in g["config"]["step_schedule"]
+    assert all(p["checksum_match"] for p in g["parity_sample"]), g["parity_sample"]
+    for k in range(2):
+        one = _bench("--seed-offset", str(k), "--timed-only")
+        assert one["checksums"][0] == g["checksums"][k], k
+
+
+def test_native_exchange_world1_stream_of_rounds():
+    """The torchrun path with a one-rank RCCL group (--exchange-world1): the exchange lanes (bsq_xchg) run beside
+    the stream of rounds and the records are those of the launcher-free run."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--exchange-world1", "--timed-only"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "bsq_xchg" in x["exchange"]["path"] and x["exchange"]["lanes"] == 4
+    assert "stream of batch runs" in x["config"]["step_schedule"]
+    one = _bench("--timed-only")
+    assert x["checksums"] == one["checksums"]
