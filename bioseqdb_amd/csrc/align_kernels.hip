@@ -332,7 +332,11 @@ DEV void ks_introsort(A a, int n, LT lt, S stk)
                 // stops; the explicit bound keeps the compiler from miscompiling this loop when `a` is a
                 // lane-interleaved index array (k_extend with S = 64 scratch hung deterministically on an unbounded
                 // scan and never with S = 1; with the bound both are exact)
+#ifdef BSQ_INTROSORT_UNBOUNDED   // tools/hang_isa.sh only: klib's scan exactly as written (sentinel a[t] == rp)
+                do ++i; while (lt(a[i], rp));
+#else
                 do ++i; while (i < t && lt(a[i], rp));
+#endif
                 do --j; while (i <= j && lt(rp, a[j]));
                 if (j <= i) break;
                 int x = a[i]; a[i] = a[j]; a[j] = x;
@@ -1925,3 +1929,10 @@ hipError_t launch_collect_overflow(hipStream_t st, int n, const uint32_t *status
 }
 
 }  // namespace bsq
+
+#ifdef BSQ_ISA_PROBE   // tools/hang_isa.sh: k_extend with lane-interleaved scratch, for the ISA comparison of DESIGN.md 3
+template __global__ void bsq::k_extend<true, 64>(bsq::DIndex, bsq::DOpts, bsq::Caps, const uint8_t *, const int64_t *, const int32_t *,
+                                            const int64_t *, int, const bsq::ChainDesc *, const bsq::Seed *, const int32_t *,
+                                            bsq::Reg *, int32_t *, uint32_t *, uint8_t *, bsq::Counters *, const int32_t *,
+                                            const int32_t *);
+#endif
