@@ -68,6 +68,33 @@ def traffic_for(stage: str, reads: int, config: str = "c3"):
         return None, None
 
 
+# VALU lane-instruction issue peak: 256 CUs x 4 SIMDs x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md: 157.3 TFLOPS
+# FP32 vector = this rate x 2 flops per FMA)
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# VALU instructions per ksw_extend2 DP cell in k_extend<true, 1>: the cell loop is unrolled by two and holds 59 VALU
+# (+6 SALU, +6 LDS) instructions (tools/dp_cell_isa.py counts them in the gfx950 ISA)
+EXT_VALU_PER_CELL = 29.5
+SQ_JSON = {c: os.path.join(ROOT, "profiles", f"sq_{c}.json") for c in ("c2", "c3", "c4")}
+
+
+def sq_for(config: str):
+    try:
+        return json.load(open(SQ_JSON[config]))
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def valu_roofline(cells: float, lone_ms: float, sq) -> dict:
+    """The extension's VALU roofline: the DP cells of one lone launch x VALU instructions per cell (the useful lane
+    instructions) over the launch time, against the VALU lane-issue peak; SQ lane utilisation beside it."""
+    useful = cells * EXT_VALU_PER_CELL
+    rate = useful / (lone_ms * 1e-3)
+    return {"bound": "valu", "dp_cells_per_launch": cells, "valu_per_cell": EXT_VALU_PER_CELL,
+            "achieved": round(rate / 1e12, 3), "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2), "unit": "T lane-instr/s",
+            "frac": round(rate / VALU_PEAK_LANE_OPS, 4),
+            "sq_lane_util": (sq or {}).get("valu_lane_util"), "sq_valu_busy": (sq or {}).get("valu_busy")}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -160,12 +187,24 @@ def fnv_vec(h: np.ndarray, v: np.ndarray) -> np.ndarray:
     return h
 
 
+# bsq_hit as a numpy record (np.ctypeslib on a ctypes.Structure pointer warns about its PEP 3118 format)
+HIT_DTYPE = np.dtype({"names": [f[0] for f in N.Hit._fields_],
+                      "formats": [np.dtype(f[1]) for f in N.Hit._fields_],
+                      "offsets": [getattr(N.Hit, f[0]).offset for f in N.Hit._fields_],
+                      "itemsize": ctypes.sizeof(N.Hit)})
+
+
+def hits_array(ptr, n: int) -> np.ndarray:
+    buf = (ctypes.c_uint8 * (n * ctypes.sizeof(N.Hit))).from_address(ctypes.addressof(ptr.contents))
+    return np.frombuffer(buf, dtype=HIT_DTYPE, count=n)
+
+
 def gpu_checksum_vec(H, n_reads: int, read_base: int = 0) -> int:
     """The oracle's orc_align_batch checksum (per-read FNV, summed), vectorised over reads; the batch's
     read r is read read_base + r of the oracle's run."""
     off = np.ctypeslib.as_array(H.read_off, shape=(n_reads + 1,)).astype(np.int64)
     nh = int(off[n_reads] - off[0])
-    hits = np.ctypeslib.as_array(H.hits, shape=(max(nh, 1),))[:nh] if nh else None
+    hits = hits_array(H.hits, nh) if nh else None
     ncig = int(H.n_cigar)
     cig = np.ctypeslib.as_array(H.cigar, shape=(max(ncig, 1),)) if ncig else np.zeros(1, np.uint32)
     h = fnv_vec(np.full(n_reads, 0xCBF29CE484222325, dtype=np.uint64),
@@ -283,7 +322,9 @@ def lone_launch(L, idx, opts, codes, offs, n, first_call):
         L.bsq_batch_stage_ms(wb, ms, 6)
         by = (ctypes.c_double * 6)()
         L.bsq_batch_stage_bytes(wb, by, 6)
-        return [float(x) for x in ms], [float(x) for x in by]
+        wk = (ctypes.c_double * 6)()
+        L.bsq_batch_stage_work(wb, wk, 6)
+        return [float(x) for x in ms], [float(x) for x in by], [float(x) for x in wk]
     finally:
         L.bsq_batch_free(wb)
 
@@ -352,6 +393,9 @@ def make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, iso_rea
     t, t_round = tr(dom, head["reads_per_launch"])
     roof = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s", **head,
             "traffic": t,
+            # the HBM bytes the launch really moved (PMC) per second of the same launch, as a fraction of peak
+            "traffic_frac": (round(t / (head["launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if t and head["launch_ms"] > 0 else None),
             "traffic_source": (f"{t_round} rocprofv3 PMC FETCH_SIZE + WRITE_SIZE passes of lone launches, per launch"
                                if t else "not measured for this shape"),
             "basis": ("lone launch: one batch of all the step's reads with nothing else on the GPU (HIP events on the "
@@ -798,7 +842,7 @@ def main() -> int:
         hb.phase = "isolated single-batch launch"
         iso = lone_launch(L, idx, opts, codes, offs, reads.n, first_call)
     elif S == 1:
-        iso = (list(stage_ms), list(stage_bytes))
+        iso = (list(stage_ms), list(stage_bytes), list(stage_work))
     if iso:   # the dominant kernel by its own (lone) time: with steps as a stream, the batches' last-step stages
         di = max(range(nst), key=lambda i: iso[0][i])   # overlap in whatever phase they drifted to
         dom = names[di]
@@ -845,6 +889,8 @@ def main() -> int:
                 "lone_traffic_bytes": tr(nm, reads.n)[0],
                 "lone_traffic_gbs": (round(tr(nm, reads.n)[0] / (iso[0][i] * 1e-3) / 1e9, 2)
                                      if iso and tr(nm, reads.n)[0] and iso[0][i] > 0 else None),
+                "lone_traffic_frac": (round(tr(nm, reads.n)[0] / (iso[0][i] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if iso and tr(nm, reads.n)[0] and iso[0][i] > 0 else None),
                 "work": float(stage_work[i]),
             } for i, nm in enumerate(names[:nst])
         },
@@ -856,6 +902,16 @@ def main() -> int:
         "index_upload_s": round(t_upload, 2),
         "retried_reads": retried,
     }
+    # SQ counters of lone launches (tools/sq_round.sh, committed under profiles/) and the extension's VALU roofline
+    sq = sq_for(args.config) if default_shape else None
+    for i, nm in enumerate(names[:nst]):
+        k = result["kernels"][STAGE_KERNEL[nm]]
+        if sq and nm in sq["stages"]:
+            st = sq["stages"][nm]
+            k["sq"] = {x: st[x] for x in ("valu_lane_util", "valu_busy", "wait_frac") if x in st}
+            k["sq"]["round"] = sq["round"]
+        if nm == "extend" and iso and len(iso) > 2 and iso[0][i] > 0:
+            k["valu"] = valu_roofline(iso[2][i], iso[0][i], k.get("sq"))
     if args.checksums and not cfg["seeding"]:
         ck = 0
         for k, b in enumerate(batches):

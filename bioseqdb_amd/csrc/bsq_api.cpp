@@ -69,8 +69,12 @@ struct RenderView {
 };
 hipError_t launch_row_len(hipStream_t, const RenderView &, int64_t *);
 hipError_t launch_row_write(hipStream_t, const RenderView &, const int64_t *, char *);
-hipError_t launch_sub_write(hipStream_t, const RenderView &, const int64_t *, char *);
-hipError_t launch_col_lens(hipStream_t, const RenderView &, int64_t *, int64_t *);
+hipError_t launch_col_class(hipStream_t, const RenderView &, int64_t *, int64_t *);
+hipError_t launch_col_holed(hipStream_t, const RenderView &, const int64_t *, int64_t, int64_t *, int64_t *, int64_t *);
+hipError_t launch_sub_write_sel(hipStream_t, const RenderView &, const int64_t *, int64_t, const int64_t *, char *);
+hipError_t launch_col_holed_size(hipStream_t, const int64_t *, int64_t, const int64_t *, int64_t *);
+hipError_t launch_col_write(hipStream_t, const RenderView &, const int64_t *, const int64_t *, const int64_t *, int64_t,
+                            const int64_t *, const uint8_t *, uint8_t *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
 hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *, int);
@@ -2421,11 +2425,10 @@ extern "C" int bsq_nuclseq_encode_batch(int device, const char *text, const int6
 }
 
 // build_tuple_bwa's two nuclseq columns for every row of the last run (extension.cpp:282-305, which calls
-// nuclseq_from_text on ref_subseq and query_subseq per row, :285,290): the subsequence texts are written
-// by the GPU renderer and encoded in place by the bulk codec; varlena 2k = ref_subseq of row k, 2k+1 =
-// its query_subseq.
-// build_tuple_bwa's two nuclseq columns of the last run's rows into the batch's pinned buffers (borrowed until the
-// next render or run of the batch): rows' texts rendered in HBM, encoded in place by the bulk codec, one D2H.
+// nuclseq_from_text on ref_subseq and query_subseq per row, :285,290) into the batch's pinned buffers (borrowed
+// until the next render or run of the batch): varlena 2k = ref_subseq of row k, 2k+1 = its query_subseq.  Texts
+// without holes are packed straight from the reference pac / the read codes (render_gpu.hip k_col_direct); the
+// few with holes are rendered as text and encoded by the bulk codec; one D2H.
 namespace bsq {
 int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **out, const int64_t **out_off)
 {
@@ -2447,46 +2450,80 @@ int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **ou
         }
     }
     hipStream_t st = b->cstream;
-    // text and pac-byte totals from the host view; the per-text offsets are computed on the device from the records
-    int64_t text_total = 0, slots = 0;
-    for (int64_t k = 0; k < H.n_hits; ++k) {
-        const bsq_hit &x = H.hits[k];
-        const int64_t l0 = x.re - x.rb, l1 = (int64_t)x.qe - x.qb;
-        text_total += l0 + l1;
-        slots += ((l0 + 3) >> 2) + ((l1 + 3) >> 2);
-    }
     b->arena.reset();
-    char *d_text;
-    int64_t *d_toff, *d_poff;
-    HIPCHK(b->arena.get(d_text, (size_t)text_total));
-    HIPCHK(b->arena.get(d_toff, (size_t)n + 1));
-    HIPCHK(b->arena.get(d_poff, (size_t)n + 1));
+    int64_t *size, *hpos;
+    HIPCHK(b->arena.get(size, (size_t)n + 1));
+    HIPCHK(b->arena.get(hpos, (size_t)n + 1));
+    uint8_t *d_out = nullptr;
+    int64_t total = 0;
+    double kms = 0;
     if (H.n_hits) {
+        // (1) hole-free texts get their varlena size directly; (2) the texts with holes (reference N runs over the
+        // window, reads with ambiguous bases) are rendered and encoded by the generic codec as a compacted subset;
+        // (3) one scan of the sizes gives every varlena's offset; (4) the hole-free varlenas are written straight from
+        // the pac / the read codes and the generic ones copied into place.
         RenderView v{};
         { const int rc = render_inputs(b, reads, v, st); if (rc) return rc; }
-        HIPCHK(launch_col_lens(st, v, d_toff, d_poff));
+        hipEvent_t ev[2];
+        for (auto &e : ev) HIPCHK(hipEventCreate(&e));
+        struct EvFree { hipEvent_t *e; ~EvFree() { hipEventDestroy(e[0]); hipEventDestroy(e[1]); } } evf{ev};
+        HIPCHK(hipEventRecord(ev[0], st));
+        HIPCHK(launch_col_class(st, v, size, hpos));
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_toff, d_toff, (int)(n + 1), st));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hpos, hpos, (int)(n + 1), st));
         uint8_t *cub = nullptr;
         HIPCHK(b->arena.get(cub, tb));
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_toff, d_toff, (int)(n + 1), st));
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, d_poff, d_poff, (int)(n + 1), st));
-        HIPCHK(launch_sub_write(st, v, d_toff, d_text));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, hpos, hpos, (int)(n + 1), st));
+        int64_t nh = 0;
+        HIPCHK(hipMemcpyAsync(&nh, hpos + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        int64_t *hl = nullptr, *enc_off = nullptr;
+        uint8_t *enc = nullptr;
+        double ekms = 0;
+        if (nh) {
+            int64_t *tl, *pl;
+            HIPCHK(b->arena.get(hl, (size_t)nh));
+            HIPCHK(b->arena.get(tl, (size_t)nh + 1));
+            HIPCHK(b->arena.get(pl, (size_t)nh + 1));
+            HIPCHK(launch_col_holed(st, v, hpos, nh, hl, tl, pl));
+            size_t tb2 = 0;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, tl, tl, (int)(nh + 1), st));
+            uint8_t *cub2 = nullptr;
+            HIPCHK(b->arena.get(cub2, tb2));
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub2, tb2, tl, tl, (int)(nh + 1), st));
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub2, tb2, pl, pl, (int)(nh + 1), st));
+            int64_t tot[2] = {0, 0};
+            HIPCHK(hipMemcpyAsync(&tot[0], tl + nh, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&tot[1], pl + nh, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            char *d_text;
+            HIPCHK(b->arena.get(d_text, (size_t)std::max<int64_t>(tot[0], 1)));
+            HIPCHK(launch_sub_write_sel(st, v, hl, nh, tl, d_text));
+            int64_t etotal = 0;
+            unsigned long long first_bad = ~0ull;
+            { const int rc = encode_device_core(st, b->arena, reinterpret_cast<const uint8_t *>(d_text), tl, pl, tot[1], nh,
+                                                false, &enc, &enc_off, &etotal, &first_bad, &ekms);
+              if (rc) return rc; }
+            HIPCHK(launch_col_holed_size(st, hl, nh, enc_off, size));
+        }
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(cub, tb, size, size, (int)(n + 1), st));
+        HIPCHK(hipMemcpyAsync(&total, size + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(b->arena.get(d_out, (size_t)std::max<int64_t>(total, 1)));
+        HIPCHK(launch_col_write(st, v, size, hpos, hl, nh, enc_off, enc, d_out));
+        HIPCHK(hipEventRecord(ev[1], st));
+        HIPCHK(hipStreamSynchronize(st));
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev[0], ev[1]);
+        kms = ms;
+        (void)ekms;
     } else {
-        HIPCHK(hipMemsetAsync(d_toff, 0, 8, st));
-        HIPCHK(hipMemsetAsync(d_poff, 0, 8, st));
+        HIPCHK(hipMemsetAsync(size, 0, 8, st));
     }
-    uint8_t *d_out = nullptr;
-    int64_t *d_off = nullptr, total = 0;
-    unsigned long long first_bad = ~0ull;
-    double kms = 0;
-    { const int rc = encode_device_core(st, b->arena, reinterpret_cast<const uint8_t *>(d_text), d_toff, d_poff, slots, n,
-                                        false, &d_out, &d_off, &total, &first_bad, &kms);
-      if (rc) return rc; }
     { int rc = grow_pinned(b->c_host, b->c_host_cap, std::max<int64_t>(total, 1), 0); if (rc) return rc; }
     { int rc = grow_pinned(b->c_off, b->c_off_cap, n + 1, 0); if (rc) return rc; }
     if (total) HIPCHK(hipMemcpyAsync(b->c_host, d_out, (size_t)total, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(b->c_off, d_off, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->c_off, size, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     *out = b->c_host;
     *out_off = b->c_off;

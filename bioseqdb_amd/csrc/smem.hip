@@ -140,6 +140,20 @@ DEV void occ_c32w(const uint4 (&w)[2], uint64_t k, bool none, int c, const SupBl
     cg = (sb->gt[c] + rg) & live;
 }
 
+// 64-bit rows: a rank block of the 3 GB table (random, outside every cache).  BSQ_EXP_NT: experiment build with
+// nontemporal loads (so the blocks do not displace the k-mer table from the caches).
+DEV void ld_wblk(const uint4 *p, uint4 (&w)[2])
+{
+#ifdef BSQ_EXP_NT
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+    const v4u b = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + 1);
+    w[0] = make_uint4(a.x, a.y, a.z, a.w); w[1] = make_uint4(b.x, b.y, b.z, b.w);
+#else
+    w[0] = p[0]; w[1] = p[1];
+#endif
+}
+
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
 // used for the rank queries (x[1] forward, x[0] backward), `o` the other one.
 // Z: the type of interval sizes x[2] -- u32 also for 64-bit rows when l_pac < 2^32 (an interval size is at most
@@ -169,8 +183,8 @@ DEV void extend1(const FM<X> &fm, X a, X o, Z x2, int c, X &na, X &no, Z &nx2, u
         constexpr int SS = 6 + SUP_SHIFT;
         const X sbk = knone ? 0 : (kk >> SS), sbl = ll >> SS;
         uint4 wk[2], wl[2];
-        wk[0] = pk[0]; wk[1] = pk[1];
-        wl[0] = pl[0]; wl[1] = pl[1];
+        ld_wblk(pk, wk);
+        ld_wblk(pl, wl);
         const X base_k = fm.sup[sbk].cnt[c];
         uint32_t rck, rgk, rcl, rgl;
         occ_c32(wk, (uint32_t)kk, knone, c, rck, rgk);
@@ -239,8 +253,8 @@ DEV void ext_back2(const FM<X> &fm, X a0, Z a2, X b0, Z b2, bool da, bool hb, in
         // the k end's cnt[c] is read from the superblock table (backward extensions never need the gt sums)
         const X sa0 = kan ? 0 : (kka >> SS), sa1 = lla >> SS, sb0 = kbn ? 0 : (kkb >> SS), sb1 = llb >> SS;
         uint4 w0[2], w1[2], w2[2], w3[2];
-        if (da) { w0[0] = p0[0]; w0[1] = p0[1]; w1[0] = p1[0]; w1[1] = p1[1]; }
-        if (hb) { w2[0] = p2[0]; w2[1] = p2[1]; w3[0] = p3[0]; w3[1] = p3[1]; }
+        if (da) { ld_wblk(p0, w0); ld_wblk(p1, w1); }
+        if (hb) { ld_wblk(p2, w2); ld_wblk(p3, w3); }
         const X base_a = fm.sup[sa0].cnt[c], base_b = fm.sup[sb0].cnt[c];
         uint32_t rk, rg_, rl;
         occ_c32(w0, (uint32_t)kka, kan, c, rk, rg_);

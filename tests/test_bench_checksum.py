@@ -69,3 +69,18 @@ def test_interval_checksum_vectorised_equals_scalar():
                 h = B.fnv(h, int(v))
         exp = (exp + h) & 0xFFFFFFFFFFFFFFFF
     assert B.intv_checksum_vec(off, iv, n) == exp
+
+
+def test_roofline_fields():
+    """The line's HBM fraction of the PMC traffic (`roofline.traffic_frac`) and the extension's VALU roofline
+    (`kernels.k_ext_key+sort+k_extend.valu`): plain ratios of the figures beside them."""
+    b = _bench()
+    roof = b.make_roofline("smem", 0, [2.0] * 6, [1e9] * 6, 1000, ([4.0] * 6, [2e9] * 6, [0.0] * 6), 1000,
+                           [8000.0] * 4, lambda stage, n: (16e9, "rXX"), 1)
+    assert roof["traffic"] == 16e9
+    assert abs(roof["traffic_frac"] - 16e9 / 4e-3 / 1e9 / b.HBM_PEAK_GBS) < 1e-4
+    none = b.make_roofline("smem", 0, [2.0] * 6, [1e9] * 6, 1000, None, 1000, None, lambda stage, n: (None, None), 1)
+    assert none["traffic_frac"] is None
+    v = b.valu_roofline(1e9, 5.0, {"valu_lane_util": 0.4, "valu_busy": 0.42})
+    assert v["frac"] == round(1e9 * b.EXT_VALU_PER_CELL / 5e-3 / b.VALU_PEAK_LANE_OPS, 4)
+    assert v["sq_lane_util"] == 0.4 and v["bound"] == "valu"
