@@ -140,18 +140,11 @@ DEV void occ_c32w(const uint4 (&w)[2], uint64_t k, bool none, int c, const SupBl
     cg = (sb->gt[c] + rg) & live;
 }
 
-// 64-bit rows: a rank block of the 3 GB table (random, outside every cache).  BSQ_EXP_NT: experiment build with
-// nontemporal loads (so the blocks do not displace the k-mer table from the caches).
+// 64-bit rows: a rank block of the 3 GB table (random, outside every cache).  Plain loads: nontemporal ones (to keep
+// the k-mer table cached) measured 21 % slower at C4.
 DEV void ld_wblk(const uint4 *p, uint4 (&w)[2])
 {
-#ifdef BSQ_EXP_NT
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
-    const v4u b = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + 1);
-    w[0] = make_uint4(a.x, a.y, a.z, a.w); w[1] = make_uint4(b.x, b.y, b.z, b.w);
-#else
     w[0] = p[0]; w[1] = p[1];
-#endif
 }
 
 // bwt_extend restricted to base c: returns (x_new_side, x_other_side, x2).  `a` is the interval end
@@ -461,41 +454,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
     if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
     int nc = 0, j = 0;
     Z last_x2 = 0;
-#ifdef BSQ_EXP_PF
-    // BSQ_EXP_PF (experiment build): the rank blocks of the next entry pair of the same position are loaded one trip
-    // early (a dword each, carried to the next trip and folded into a sink there), so their lines are in the caches
-    // when that trip's real loads issue: two pairs' round trips in flight instead of one.
-    uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf_sink = 0;
-#endif
-#ifdef BSQ_EXP_PF2
-    // and the blocks of the next position's first two entries as they are written (folded at the position switch)
-    uint32_t pn0 = 0, pn1 = 0, pn2 = 0, pn3 = 0;
-#endif
     for (;;) {
         {
-#ifdef BSQ_EXP_PF
-            pf_sink ^= pf0 ^ pf1 ^ pf2 ^ pf3;
-            pf0 = pf1 = pf2 = pf3 = 0;
-            if (c >= 0 && j + 2 < n) {
-                X r0; Z r2; int re_;
-                L.get(j + 2, r0, r2, re_);
-                if (re_ - i > K) {
-                    const X k = r0 - 1, l = r0 - 1 + (X)r2;
-                    const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-                    pf0 = reinterpret_cast<const uint32_t *>(fm.occ32 + (k == (X)-1 ? 0 : (kk >> 6)))[0];
-                    pf1 = reinterpret_cast<const uint32_t *>(fm.occ32 + (ll >> 6))[0];
-                }
-                if (j + 3 < n) {
-                    L.get(j + 3, r0, r2, re_);
-                    if (re_ - i > K) {
-                        const X k = r0 - 1, l = r0 - 1 + (X)r2;
-                        const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-                        pf2 = reinterpret_cast<const uint32_t *>(fm.occ32 + (k == (X)-1 ? 0 : (kk >> 6)))[0];
-                        pf3 = reinterpret_cast<const uint32_t *>(fm.occ32 + (ll >> 6))[0];
-                    }
-                }
-            }
-#endif
             // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
             // Compaction writes go to nc <= j, below both entries already read.
             const bool hb = j + 1 < n;
@@ -535,15 +495,6 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
                         last_start = i + 1;
                     }
                 } else if (nc == 0 || o2 != last_x2) {
-#ifdef BSQ_EXP_PF2
-                    if (nc < 2 && pe - (i - 1) > K) {   // its rank blocks at position i - 1 (base-independent rows)
-                        const X k = o0 - 1, l = o0 - 1 + (X)o2;
-                        const X kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-                        const uint32_t a = reinterpret_cast<const uint32_t *>(fm.occ32 + (k == (X)-1 ? 0 : (kk >> 6)))[0];
-                        const uint32_t b = reinterpret_cast<const uint32_t *>(fm.occ32 + (ll >> 6))[0];
-                        if (nc == 0) { pn0 = a; pn1 = b; } else { pn2 = a; pn3 = b; }
-                    }
-#endif
                     L.set(nc++, o0, o2, pe);
                     last_x2 = o2;
                 }
@@ -552,20 +503,12 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
         j += 2;
         if (j >= n) {   // position i done (at i = -1 every entry is a hit, so nc == 0 ends the loop there)
             if (nc == 0) break;
-#ifdef BSQ_EXP_PF2
-            pf_sink ^= pn0 ^ pn1 ^ pn2 ^ pn3;
-            pn0 = pn1 = pn2 = pn3 = 0;
-#endif
             n = nc; nc = 0; j = 0; last_x2 = 0;
             --i;
             c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
             if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
         }
     }
-#ifdef BSQ_EXP_PF
-    pf_sink ^= pf0 ^ pf1 ^ pf2 ^ pf3;
-    if (pf_sink == 0x6a09e667u) nblk ^= 1;   // keeps the early loads (a statistics counter only, never a result)
-#endif
     return ret;
 }
 
