@@ -4,7 +4,7 @@
 tag=$1; var=$2; a=$3; b=$4; cfg=${5:-c3}; ns=${6:-1}; out=gpurun_out/$tag; mkdir -p $out
 for rep in 1 2; do
   for v in $a $b; do
-    env $var=$v timeout -k 10 300 python bench.py --config $cfg --timed-only --streams $ns --steps 3 --warmup 1 > $out/ab_${v}_$rep.json 2> $out/ab_${v}_$rep.err || exit 1
+    env $var=$v timeout -k 10 300 python bench.py --config $cfg --timed-only --streams $ns --steps ${STEPS:-3} --warmup 1 > $out/ab_${v}_$rep.json 2> $out/ab_${v}_$rep.err || exit 1
     python3 -c "import json,sys; d=json.load(open('$out/ab_${v}_$rep.json')); print('$var=$v', d['value'], d['ms_per_step'], d['stages_ms'])"
   done
 done
