@@ -1549,7 +1549,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
                                                            int n, const ChainDesc *chains, const Seed *seeds,
                                                            const int32_t *n_chains, Reg *regs_out, int32_t *n_regs,
                                                            uint32_t *status, uint8_t *scratch, Counters *ctr,
-                                                           const int32_t *order, const int32_t *sscore)
+                                                           const int32_t *order, const int32_t *sscore, int32_t *work)
 {
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1568,10 +1568,10 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     X.eh = SP<int2, S>{reinterpret_cast<int2 *>(wb + off) + lane};
     off += (size_t)(cp.max_len + 2) * S * sizeof(int2);
     X.stk = SP<int, S>{reinterpret_cast<int *>(wb + off) + lane};
-    for (int it = tid; it < n; it += nthr) {
+    auto one = [&](int it) {
         const int li = order ? order[it] : it;   // reads ordered by estimated extension work (lane balance)
         n_regs[li] = 0;
-        if (status[li]) continue;
+        if (status[li]) return;
         const int r = read_of(sel, li);
         const uint8_t *q = codes + offs[r];
         const int len = (int)(offs[r + 1] - offs[r]);
@@ -1594,10 +1594,24 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
             for (int c = 0; c < nc && !X.ovf; ++c)
                 chain2aln(ix, o, len, q, cd[c], sd + cd[c].seed_off, ss ? ss + cd[c].seed_off : nullptr, X, ehx, qm, cells, bases);
         }
-        if (X.ovf) { status[li] |= ST_OVERFLOW; continue; }
+        if (X.ovf) { status[li] |= ST_OVERFLOW; return; }
         X.n = sort_dedup_patch(ix, o, q, X, cells, bases);
         mark_primary_se(o, X, ids[r]);
         n_regs[li] = X.n;
+    };
+    // With a work counter each wave takes the next 64 reads of the order, heaviest first (the order is ascending in
+    // estimated work): neighbouring reads carry similar work (lane balance), and the light chunks at the end fill in
+    // behind the waves that drew heavy ones instead of leaving a tail.  Without one (the retry pass), a fixed stride.
+    // One call site of the body either way.
+    for (int it = tid;; it += nthr) {
+        if (work) {
+            int base = 0;
+            if ((threadIdx.x & 63) == 0) base = atomicAdd(work, 64);   // one vector atomic per 64 reads
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base >= n) break;
+            it = n - 1 - (base + (int)(threadIdx.x & 63));   // < 0 past the last read
+        } else if (it >= n) break;
+        if (it >= 0 && it < n) one(it);
     }
     wave_add(&ctr[STG_EXTEND].dp_cells, cells);
     wave_add(&ctr[STG_EXTEND].ref_bases, bases);
@@ -1853,7 +1867,7 @@ hipError_t launch_ext_key(hipStream_t st, const Caps &cp, const int64_t *offs, c
 hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                          const int64_t *offs, const int32_t *sel, const int64_t *ids, int n, const ChainDesc *chains,
                          const Seed *seeds, const int32_t *n_chains, Reg *regs, int32_t *n_regs, uint32_t *status,
-                         uint8_t *scratch, Counters *ctr, const int32_t *order, const int32_t *sscore)
+                         uint8_t *scratch, Counters *ctr, const int32_t *order, const int32_t *sscore, int32_t *work)
 {
     // LDS row storage when the u16 bound holds: h, e <= h0 + qlen*max with h0 <= len*a (+ a left score)
     // and the 64-column ring holds the band: ksw_extend2 clamps w to max_ins/max_del (ksw.c), which for
@@ -1872,13 +1886,17 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     // Contiguous per-thread scratch (S = 1).  The lane-interleaved layout (S = 64, as k_chain's) measured slower
     // here: lone 1M-read launch 7.0 ms against 6.67 ms, PMC fetch + write 1.17 GB against 1.28 GB -- the kernel is
     // bound by VALU issue under divergence, not by its scratch traffic.
+    if (work) {
+        const hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+    }
     if (lds) {
         const size_t sh = (size_t)64 * EXT_LDS_COLS * 4 + (size_t)64 * (cp.max_len + 2);
         hipLaunchKernelGGL((k_extend<true, 1>), dim3(grid * 4), dim3(64), sh, st, ix, o, cp, codes, offs, sel, ids, n,
-                           chains, seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
+                           chains, seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore, work);
     } else {
         hipLaunchKernelGGL((k_extend<false, 1>), dim3(grid), dim3(256), 0, st, ix, o, cp, codes, offs, sel, ids, n, chains,
-                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore);
+                           seeds, n_chains, regs, n_regs, status, scratch, ctr, order, sscore, work);
     }
     return hipGetLastError();
 }
@@ -1934,5 +1952,5 @@ hipError_t launch_collect_overflow(hipStream_t st, int n, const uint32_t *status
 template __global__ void bsq::k_extend<true, 64>(bsq::DIndex, bsq::DOpts, bsq::Caps, const uint8_t *, const int64_t *, const int32_t *,
                                             const int64_t *, int, const bsq::ChainDesc *, const bsq::Seed *, const int32_t *,
                                             bsq::Reg *, int32_t *, uint32_t *, uint8_t *, bsq::Counters *, const int32_t *,
-                                            const int32_t *);
+                                            const int32_t *, int32_t *);
 #endif

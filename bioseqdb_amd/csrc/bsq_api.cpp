@@ -35,7 +35,7 @@ hipError_t launch_chain(int, hipStream_t, const DIndex &, const DOpts &, const C
                         Counters *);
 hipError_t launch_extend(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                          const int32_t *, const int64_t *, int, const ChainDesc *, const Seed *, const int32_t *, Reg *,
-                         int32_t *, uint32_t *, uint8_t *, Counters *, const int32_t *, const int32_t *);
+                         int32_t *, uint32_t *, uint8_t *, Counters *, const int32_t *, const int32_t *, int32_t *);
 hipError_t launch_flt_seeds(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                             const int32_t *, int, ChainDesc *, Seed *, const int32_t *, const uint32_t *, int32_t *,
                             uint8_t *, Counters *);
@@ -168,6 +168,8 @@ extern "C" int bsq_device_count(void)
 
 // BSQ_R2A_DIAG=0: no lane-per-read diagonal pass before the reg2aln group kernels (A/B measurements)
 static bool no_r2a_diag() { const char *e = getenv("BSQ_R2A_DIAG"); return e && *e == '0'; }
+// BSQ_EXT_STATIC=1: k_extend takes its reads by a fixed stride instead of a work counter (A/B measurements)
+static bool ext_static() { static const bool v = [] { const char *e = getenv("BSQ_EXT_STATIC"); return e && *e == '1'; }(); return v; }
 static bool tiny_caps() { const char *e = getenv("BSQ_TEST_TINY_CAPS"); return e && *e && *e != '0'; }
 
 static int default_threads()
@@ -802,7 +804,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.zslab, (size_t)w.zslab_blocks * 4 * (size_t)w.zslab_bytes));
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
-        HIPCHK(hipMalloc(&w.dcount, 16));
+        HIPCHK(hipMalloc(&w.dcount, 32));   // launch_reg2aln_chain's 5 counters, then k_extend's work counter
         HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 4)));
         if (cp.max_len <= 1024) HIPCHK(hipMalloc(&w.codes_t, (size_t)intv_slot_reads((int64_t)R) * (size_t)cp.max_len));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
@@ -1261,7 +1263,8 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         order = w.eidx1;
     }
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,
-                         w.n_regs, w.status, w.scratch, b->ctr, order, w.sscore));
+                         w.n_regs, w.status, w.scratch, b->ctr, order, w.sscore,
+                         w.dcount && !ext_static() ? w.dcount + 5 : nullptr));
     if (timed) HIPCHK(hipEventRecord(b->ev[STG_REG2ALN], st));
     rg.next("reg2aln");
     if (!sel && w.cp.max_len <= 1024) {

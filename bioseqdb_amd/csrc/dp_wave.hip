@@ -12,6 +12,7 @@
 // Integer arithmetic only; results equal the serial ksw_global2 cell for cell.
 // Restates algorithms of BWA (lh3/bwa, Apache-2.0) and klib (MIT) for bit-exact results; see NOTICE.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "bsq_device.h"
@@ -414,7 +415,7 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
                                                    int32_t *__restrict__ n_cig_read, uint32_t *__restrict__ status,
                                                    Counters *ctr, int zcap, uint8_t *__restrict__ zslab,
                                                    int64_t zslab_bytes, const int32_t *__restrict__ list,
-                                                   const int32_t *__restrict__ list_n)
+                                                   const int32_t *__restrict__ list_n, int32_t *__restrict__ work)
 {
     // the control below is wave-uniform: make that visible so it lives in SGPRs / scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -429,7 +430,16 @@ __global__ void __launch_bounds__(256) k_reg2aln_w(DIndex ix, DOpts o, Caps cp, 
     uint8_t *z_glob = zslab + (size_t)gw * (size_t)zslab_bytes;   // this wave's spill slab
     uint64_t cells = 0, bases = 0;
     const int n_items = list ? *list_n : n;   // reads deferred by the group kernels, or all reads
-    for (int it_ = gw; it_ < n_items; it_ += nw) {
+    // Reads are taken from a work counter, one per wave at a time: their cost varies by 10x and more (bands of 33-77
+    // columns, one to three band doublings, one or two regions), so a fixed stride left the launch waiting on the waves
+    // that drew the expensive ones.  (work == nullptr: fixed stride.)
+    auto next = [&](int cur) -> int {
+        if (!work) return cur + nw;
+        int v = 0;
+        if (lane_id() == 0) v = atomicAdd(work, 1);   // one vector atomic per read
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    for (int it_ = work ? next(0) : gw; it_ < n_items; it_ = next(it_)) {
     const int li = list ? list[it_] : it_;
     if (status[li]) { n_cig_read[li] = 0; continue; }
     {
@@ -513,7 +523,7 @@ hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, co
                             const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
                             uint32_t *cigars, int32_t *n_cig, uint32_t *status, Counters *ctr, int zcap,
                             uint8_t *zslab, int64_t zslab_bytes, int max_blocks, const int32_t *list,
-                            const int32_t *list_n)
+                            const int32_t *list_n, int32_t *work)
 {
     const int waves = 4;
     int grid = (n + waves - 1) / waves;
@@ -522,8 +532,12 @@ hipError_t launch_reg2aln_w(hipStream_t st, const DIndex &ix, const DOpts &o, co
     const size_t eh_bytes = ((size_t)(cp.max_len + 2) * sizeof(int2) + 15) & ~(size_t)15;
     const size_t q_bytes = ((size_t)cp.max_len + 16) & ~(size_t)15;
     const size_t sh = (size_t)waves * (eh_bytes + (size_t)zcap + q_bytes);
+    if (work) {
+        const hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_reg2aln_w, dim3(grid), dim3(64 * waves), sh, st, ix, o, cp, codes, offs, n, regs, n_regs, hits,
-                       cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes, list, list_n);
+                       cigars, n_cig, status, ctr, zcap, zslab, zslab_bytes, list, list_n, work);
     return hipGetLastError();
 }
 
@@ -1013,8 +1027,12 @@ __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps c
     wave_add(&ctr[STG_REG2ALN].ref_bases, bases);
 }
 
+// BSQ_R2A_STATIC=1: the whole-wave kernel takes its reads by a fixed stride (A/B measurements)
+static bool r2a_static() { static const bool v = [] { const char *e = getenv("BSQ_R2A_STATIC"); return e && *e == '1'; }(); return v; }
+
 // group kernels G = 16 then 32 over the reads (in `order` when given), the whole-wave kernel over what remains
-// dn: 4 counters -- [0], [1] the group kernels' defer lists, [3] the diagonal pass's ([2] is order_n's home);
+// dn: 5 counters -- [0], [1] the group kernels' defer lists, [3] the diagonal pass's ([2] is order_n's home), [4] the
+// whole-wave kernel's work counter;
 // pre: n entries for the diagonal pass's list (nullptr: no diagonal pass)
 hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
                                 const int64_t *offs, int n, const Reg *regs, const int32_t *n_regs, Hit *hits,
@@ -1041,7 +1059,7 @@ hipError_t launch_reg2aln_chain(hipStream_t st, const DIndex &ix, const DOpts &o
                      zcap, max_blocks);
     if (e != hipSuccess) return e;
     return launch_reg2aln_w(st, ix, o, cp, codes, offs, n, regs, n_regs, hits, cigars, n_cig, status, ctr, zcap, zslab,
-                            zslab_bytes, max_blocks, d1, dn + 1);
+                            zslab_bytes, max_blocks, d1, dn + 1, r2a_static() ? nullptr : dn + 4);
 }
 
 }  // namespace bsq
