@@ -805,7 +805,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dlist0, R * 4));
         HIPCHK(hipMalloc(&w.dlist1, R * 4));
         HIPCHK(hipMalloc(&w.dcount, 32));   // launch_reg2aln_chain's 5 counters, then k_extend's work counter
-        HIPCHK(hipMalloc(&w.lspill, R * LSPILL * (2 * 8 + 4)));
+        HIPCHK(hipMalloc(&w.lspill, (size_t)intv_slot_reads((int64_t)R) * LSPILL * (2 * 8 + 4)));   // whole waves
         if (cp.max_len <= 1024) HIPCHK(hipMalloc(&w.codes_t, (size_t)intv_slot_reads((int64_t)R) * (size_t)cp.max_len));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
         HIPCHK(hipMalloc(&w.ekey1, R * 4));

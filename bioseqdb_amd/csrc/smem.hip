@@ -270,7 +270,8 @@ DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
 
 // The lane's list of (x0, x2, end) entries: entries e < cap in LDS (entry e at element offset e * stride,
 // lane-interleaved), the next gcap in this read's global spill area (lists longer than the LDS share
-// are rare; they cost global accesses instead of a retry).  The LDS part is addressed by offsets into the
+// cost global accesses instead of a retry; the spill area is wave-interleaved too, entry g of a lane at
+// [g * 64], so the lanes of a wave that spill the same entry share lines).  The LDS part is addressed by offsets into the
 // dynamic LDS arrays and the spill part is read with (relaxed, wave-scope) atomic loads, so the compiler
 // cannot merge the two branches' loads into one flat load through a selected pointer: flat loads of LDS
 // go through the vector memory pipeline and make every wait cover both counters.
@@ -294,12 +295,12 @@ struct LList {
     DEV void set(int e, X a, Z b, int en)
     {
         if (e < cap) { lds_x<X>(x0 + e * stride) = a; lds_x<Z>(x2 + e * stride) = b; g_smem_u16[end + e * stride] = (uint16_t)en; }
-        else { const int g = e - cap; gx0[g] = a; gx2[g] = b; gend[g] = (uint32_t)en; }
+        else { const int g = (e - cap) * 64; gx0[g] = a; gx2[g] = b; gend[g] = (uint32_t)en; }
     }
     DEV void get(int e, X &a, Z &b, int &en) const
     {
         if (e < cap) { a = lds_x<X>(x0 + e * stride); b = lds_x<Z>(x2 + e * stride); en = g_smem_u16[end + e * stride]; }
-        else { const int g = e - cap; a = spill_load(gx0 + g); b = spill_load(gx2 + g); en = (int)spill_load(gend + g); }
+        else { const int g = (e - cap) * 64; a = spill_load(gx0 + g); b = spill_load(gx2 + g); en = (int)spill_load(gend + g); }
     }
 };
 
@@ -607,8 +608,10 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     L.end = (int)((size_t)T * lcap * (sizeof(X) + sizeof(Z)) / 2) + t;
     L.stride = T;
     L.cap = lcap;
-    {   // spill area: [x0: n*gcap X][x2: n*gcap Z][end: n*gcap u32], this read's gcap entries of each
-        const size_t me = (size_t)(blockIdx.x * T + t) * (size_t)gcap, tot = (size_t)n * (size_t)gcap;
+    {   // spill area: [x0: N*gcap X][x2: N*gcap Z][end: N*gcap u32] (N = n in whole waves), each array holding a
+        // wave's gcap entries per lane lane-interleaved (entry g of lane l at [g * 64 + l] of the wave's block)
+        const size_t li0 = (size_t)blockIdx.x * T + t;
+        const size_t me = (li0 >> 6) * 64 * (size_t)gcap + (li0 & 63), tot = (size_t)(n + 63) / 64 * 64 * (size_t)gcap;
         L.gx0 = reinterpret_cast<X *>(spill) + me;
         L.gx2 = reinterpret_cast<Z *>(spill + tot * sizeof(X)) + me;
         L.gend = reinterpret_cast<uint32_t *>(spill + tot * (sizeof(X) + sizeof(Z))) + me;
