@@ -518,7 +518,7 @@ template <int S>
 __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, const int64_t *offs, const int32_t *sel,
                                                int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains_out,
                                                Seed *seeds_out, int32_t *n_chains, uint32_t *status,
-                                               uint8_t *scratch, Counters *ctr)
+                                               uint8_t *scratch, Counters *ctr, int only_marked)
 {
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -542,6 +542,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
     SP<int, S> kept_list = ord + cp.chains;
     SP<int, S> stk = kept_list + cp.chains;   // introsort stack (192 ints), then the B-tree walk's (3 x 24)
     for (int li = tid; li < n; li += nthr) {
+        if (only_marked && n_chains[li] != -1) continue;   // second launch after k_chain_s: the reads it left
         n_chains[li] = 0;
         if (status[li]) continue;
         const int r = read_of(sel, li);
@@ -667,6 +668,239 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
                 for (int s = c.head; s >= 0; s = C.seeds[s].next) {
                     so[ns].rbeg = C.seeds[s].rbeg; so[ns].qbeg = C.seeds[s].qbeg; so[ns].len = C.seeds[s].len;
                     ++ns;
+                }
+                ++nc;
+            }
+            n_chains[li] = nc;
+        }
+    }
+    wave_add(&ctr[STG_CHAIN].sa_values, nsa);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_chain_s: mem_chain + mem_chain_flt for the reads whose chaining state fits a small LDS share: at most CS_NS
+// seeds and CS_NC chains, i.e. a kbtree that never grows past its root leaf (the 10th key splits it).  The state
+// lives in LDS, lane-interleaved (one-wave blocks), instead of k_chain's global scratch, so the tree operations
+// and the chain filter cost LDS round trips and no memory traffic; the intervals of four MEMs and their first SA
+// values are loaded together (one round trip each instead of one per MEM).  On the root leaf kbtree reduces to a
+// sorted key array: kb_intervalp_lower returns the first key whose pos equals the probe, else the last one below
+// it; kb_putp inserts after the first key not below the probe (after the first equal one).  A read that outgrows
+// the share is marked (n_chains = -1) and chained from scratch by k_chain<64>'s second launch (launch_chain).
+// ------------------------------------------------------------------------------------------------
+constexpr int CS_NS = 12, CS_NC = 2 * KB_T - 1;
+extern __shared__ uint8_t g_lds_cs[];
+
+struct CsLds {   // element e of lane l of an array of element size z: base + (e * 64 + l) * z
+    static constexpr int RB = 0;                      // i64 seed rbeg
+    static constexpr int QL = RB + CS_NS * 64 * 8;    // u32 seed qbeg | len << 16
+    static constexpr int NX = QL + CS_NS * 64 * 4;    // u8 seed next (0xff: last)
+    static constexpr int CW = NX + CS_NS * 64;        // i32 chain w
+    static constexpr int CR = CW + CS_NC * 64 * 4;    // i32 chain rid
+    static constexpr int CH = CR + CS_NC * 64 * 4;    // u8 chain head, tail, n, kept, first (i8), then the leaf's
+    static constexpr int CT = CH + CS_NC * 64;        // keys, ord and the kept list
+    static constexpr int CN = CT + CS_NC * 64;
+    static constexpr int CK = CN + CS_NC * 64;
+    static constexpr int CF = CK + CS_NC * 64;
+    static constexpr int LF = CF + CS_NC * 64;
+    static constexpr int OR = LF + CS_NC * 64;
+    static constexpr int KL = OR + CS_NC * 64;
+    static constexpr int BYTES = KL + CS_NC * 64;
+    int l;
+    DEV int64_t &rb(int e) const { return *reinterpret_cast<int64_t *>(g_lds_cs + RB + (e * 64 + l) * 8); }
+    DEV uint32_t &ql(int e) const { return *reinterpret_cast<uint32_t *>(g_lds_cs + QL + (e * 64 + l) * 4); }
+    DEV uint8_t &nx(int e) const { return g_lds_cs[NX + e * 64 + l]; }
+    DEV int32_t &cw(int c) const { return *reinterpret_cast<int32_t *>(g_lds_cs + CW + (c * 64 + l) * 4); }
+    DEV int32_t &cr(int c) const { return *reinterpret_cast<int32_t *>(g_lds_cs + CR + (c * 64 + l) * 4); }
+    DEV uint8_t &ch(int c) const { return g_lds_cs[CH + c * 64 + l]; }
+    DEV uint8_t &ct(int c) const { return g_lds_cs[CT + c * 64 + l]; }
+    DEV uint8_t &cn(int c) const { return g_lds_cs[CN + c * 64 + l]; }
+    DEV uint8_t &ck(int c) const { return g_lds_cs[CK + c * 64 + l]; }
+    DEV int8_t &cf(int c) const { return reinterpret_cast<int8_t &>(g_lds_cs[CF + c * 64 + l]); }
+    DEV uint8_t &lf(int i) const { return g_lds_cs[LF + i * 64 + l]; }
+    DEV int qb(int e) const { return (int)(ql(e) & 0xffffu); }
+    DEV int ln(int e) const { return (int)(ql(e) >> 16); }
+};
+
+struct CsIdx {   // an index array of CsLds (ord, kept list) for ks_introsort
+    int off;
+    DEV uint8_t &operator[](int i) const { return g_lds_cs[off + i * 64]; }
+    DEV CsIdx operator+(int i) const { return CsIdx{off + i * 64}; }
+};
+
+// lower_bound of kpos over the leaf's keys by chain pos (the pos of a chain is its first seed's rbeg)
+DEV int cs_lower(const CsLds &L, int nk, int64_t kpos)
+{
+    int lo = 0, hi = nk;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (L.rb(L.ch(L.lf(mid))) < kpos) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(64) k_chain_s(DIndex ix, DOpts o, Caps cp, const int64_t *offs, int n, const Intv *intv,
+                                                const int32_t *n_intv, ChainDesc *chains_out, Seed *seeds_out,
+                                                int32_t *n_chains, const uint32_t *status, Counters *ctr)
+{
+    const int nthr = gridDim.x * 64, tid = blockIdx.x * 64 + threadIdx.x;
+    const CsLds L{(int)threadIdx.x};
+    const int NS = cp.seeds < CS_NS ? cp.seeds : CS_NS, NC = cp.chains < CS_NC ? cp.chains : CS_NC;
+    uint64_t nsa = 0;
+    for (int li = tid; li < n; li += nthr) {
+        n_chains[li] = 0;
+        if (status[li]) continue;
+        const int len = (int)(offs[li + 1] - offs[li]);
+        if (len < o.min_seed_len) continue;
+        bool big = len > 0xffff;   // qbeg and len are kept in 16 bits
+        int ns = 0, nk = 0;        // seeds; chains (= the keys of the root leaf)
+        uint64_t rsa = 0;
+        const SP<const Intv> mem{intv + intv_slot_at_d(li, 0, cp.intv)};
+        const int nm = n_intv[li];
+        for (int i0 = 0; i0 < nm && !big; i0 += 4) {
+            uint64_t a0[4], a2[4], ai[4], s0[4];   // x[0], x[2], info and the first SA value of MEMs i0 .. i0 + 3
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a0[u] = a2[u] = ai[u] = 0;
+                if (i0 + u < nm) { const Intv &m = mem[i0 + u]; a0[u] = m.x[0]; a2[u] = m.x[2]; ai[u] = m.info; }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s0[u] = a2[u] > 0 ? sa_at(ix, a0[u]) : 0;
+            const int ue = nm - i0 < 4 ? nm - i0 : 4;
+            for (int u = 0; u < ue && !big; ++u) {
+                const uint64_t px0 = u == 0 ? a0[0] : u == 1 ? a0[1] : u == 2 ? a0[2] : a0[3];
+                const uint64_t px2 = u == 0 ? a2[0] : u == 1 ? a2[1] : u == 2 ? a2[2] : a2[3];
+                const uint64_t pin = u == 0 ? ai[0] : u == 1 ? ai[1] : u == 2 ? ai[2] : ai[3];
+                const uint64_t sa0 = u == 0 ? s0[0] : u == 1 ? s0[1] : u == 2 ? s0[2] : s0[3];
+                const int slen = (int)((uint32_t)pin - (uint32_t)(pin >> 32));
+                const int qbeg = (int)(pin >> 32);
+                const int step = px2 > (uint64_t)o.max_occ ? (int)(px2 / (uint64_t)o.max_occ) : 1;
+                int count = 0;
+                for (int64_t k = 0; (uint64_t)k < px2 && count < o.max_occ && !big; k += step, ++count) {
+                    const int64_t rbeg = (int64_t)(k == 0 ? sa0 : sa_at(ix, px0 + (uint64_t)k));
+                    ++rsa;
+                    const int rid = intv2rid(ix, rbeg, rbeg + slen);
+                    if (rid < 0) continue;
+                    bool to_add = true;
+                    if (nk) {
+                        const int lo = cs_lower(L, nk, rbeg);
+                        const int lower = lo < nk && L.rb(L.ch(L.lf(lo))) == rbeg ? L.lf(lo) : lo > 0 ? L.lf(lo - 1) : -1;
+                        if (lower >= 0 && rid == L.cr(lower)) {   // test_and_merge
+                            const int hd = L.ch(lower), tl = L.ct(lower);
+                            const int64_t frb = L.rb(hd), lrb = L.rb(tl);
+                            const int fqb = L.qb(hd), lqb = L.qb(tl), lln = L.ln(tl);
+                            const int64_t qend = lqb + lln, rend = lrb + lln;
+                            if (qbeg >= fqb && qbeg + slen <= qend && rbeg >= frb && rbeg + slen <= rend) {
+                                to_add = false;   // contained
+                            } else if (!((lrb < ix.l_pac || frb < ix.l_pac) && rbeg >= ix.l_pac)) {
+                                const int64_t x = qbeg - lqb, y = rbeg - lrb;
+                                if (y >= 0 && x - y <= o.w && y - x <= o.w && x - lln < o.max_chain_gap &&
+                                    y - lln < o.max_chain_gap) {
+                                    to_add = false;
+                                    if (ns >= NS) { big = true; break; }
+                                    const int si = ns++;
+                                    L.rb(si) = rbeg; L.ql(si) = (uint32_t)qbeg | (uint32_t)slen << 16; L.nx(si) = 0xff;
+                                    L.nx(tl) = (uint8_t)si;
+                                    L.ct(lower) = (uint8_t)si;
+                                    L.cn(lower) = (uint8_t)(L.cn(lower) + 1);
+                                }
+                            }
+                        }
+                    }
+                    if (to_add) {
+                        if (nk >= NC || ns >= NS) { big = true; break; }
+                        const int si = ns++, ci = nk;
+                        L.rb(si) = rbeg; L.ql(si) = (uint32_t)qbeg | (uint32_t)slen << 16; L.nx(si) = 0xff;
+                        L.cr(ci) = rid; L.cn(ci) = 1; L.ch(ci) = L.ct(ci) = (uint8_t)si; L.cw(ci) = 0; L.ck(ci) = 0; L.cf(ci) = -1;
+                        // kb_putp on the leaf: after the first key not below rbeg if it equals rbeg, else before it
+                        const int lo = nk ? cs_lower(L, nk, rbeg) : 0;
+                        const int at = nk == 0 ? 0 : lo == nk ? nk : (L.rb(L.ch(L.lf(lo))) > rbeg ? lo : lo + 1);
+                        for (int j = nk - 1; j >= at; --j) L.lf(j + 1) = L.lf(j);
+                        L.lf(at) = (uint8_t)ci;
+                        ++nk;
+                    }
+                }
+            }
+        }
+        if (big) { n_chains[li] = -1; continue; }
+        nsa += rsa;
+        // in-order traversal of the leaf = its keys; mem_chain_flt
+        const CsIdx ord{CsLds::OR + L.l}, kept_list{CsLds::KL + L.l};
+        int n_chn = 0;
+        for (int i = 0; i < nk; ++i) {
+            const int ci = L.lf(i);
+            L.cf(ci) = -1; L.ck(ci) = 0;
+            int64_t end = 0;
+            int w = 0;
+            for (int e = L.ch(ci); e != 0xff; e = L.nx(e)) {
+                const int qb = L.qb(e), sl = L.ln(e);
+                if (qb >= end) w += sl;
+                else if (qb + sl > end) w += (int)(qb + sl - end);
+                end = end > qb + sl ? end : qb + sl;
+            }
+            const int tmp = w;
+            w = 0; end = 0;
+            for (int e = L.ch(ci); e != 0xff; e = L.nx(e)) {
+                const int64_t rb = L.rb(e);
+                const int sl = L.ln(e);
+                if (rb >= end) w += sl;
+                else if (rb + sl > end) w += (int)(rb + sl - end);
+                end = end > rb + sl ? end : rb + sl;
+            }
+            w = w < tmp ? w : tmp;
+            w = w < (1 << 30) ? w : (1 << 30) - 1;
+            L.cw(ci) = w;
+            if (w >= o.min_chain_weight) ord[n_chn++] = (uint8_t)ci;
+        }
+        if (n_chn > 0) {
+            ks_introsort(ord, n_chn, [L](int a, int b) { return L.cw(a) > L.cw(b); }, SP<int>{nullptr});
+            L.ck(ord[0]) = 3;
+            int nkl = 0;
+            kept_list[nkl++] = 0;
+            for (int i = 1; i < n_chn; ++i) {
+                int large_ovlp = 0, k;
+                const int ci = ord[i];
+                const int bi = L.qb(L.ch(ci)), ei = L.qb(L.ct(ci)) + L.ln(L.ct(ci));
+                for (k = 0; k < nkl; ++k) {
+                    const int j = kept_list[k], cj = ord[j];
+                    const int bj = L.qb(L.ch(cj)), ej = L.qb(L.ct(cj)) + L.ln(L.ct(cj));
+                    const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
+                    if (e_min > b_max) {   // is_alt is always 0 on this path
+                        const int li2 = ei - bi, lj = ej - bj, min_l = li2 < lj ? li2 : lj;
+                        if (e_min - b_max >= min_l * o.mask_level && min_l < o.max_chain_gap) {
+                            large_ovlp = 1;
+                            if (L.cf(cj) < 0) L.cf(cj) = (int8_t)i;
+                            if (L.cw(ci) < L.cw(cj) * o.drop_ratio && L.cw(cj) - L.cw(ci) >= o.min_seed_len << 1) break;
+                        }
+                    }
+                }
+                if (k == nkl) {
+                    kept_list[nkl++] = (uint8_t)i;
+                    L.ck(ci) = large_ovlp ? 2 : 3;
+                }
+            }
+            for (int i = 0; i < nkl; ++i) {
+                const int ci = ord[kept_list[i]];
+                if (L.cf(ci) >= 0) L.ck(ord[L.cf(ci)]) = 1;
+            }
+            int i, k;
+            for (i = k = 0; i < n_chn; ++i) {
+                const int kp = L.ck(ord[i]);
+                if (kp == 0 || kp == 3) continue;
+                if (++k >= o.max_chain_extend) break;
+            }
+            for (; i < n_chn; ++i)
+                if (L.ck(ord[i]) < 3) L.ck(ord[i]) = 0;
+            ChainDesc *cd = chains_out + (size_t)li * cp.chains;
+            Seed *so = seeds_out + (size_t)li * cp.seeds;
+            int nc = 0, nso = 0;
+            for (i = 0; i < n_chn; ++i) {
+                const int ci = ord[i];
+                if (L.ck(ci) == 0) continue;
+                cd[nc].seed_off = nso; cd[nc].n = L.cn(ci); cd[nc].rid = L.cr(ci); cd[nc].w = L.cw(ci);
+                for (int e = L.ch(ci); e != 0xff; e = L.nx(e)) {
+                    so[nso].rbeg = L.rb(e); so[nso].qbeg = L.qb(e); so[nso].len = L.ln(e);
+                    ++nso;
                 }
                 ++nc;
             }
@@ -1554,9 +1788,9 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t cells = 0, bases = 0;
-    // S = 64: this wave's 64 * cp.scratch bytes, each array lane-interleaved; S = 1: the thread's own bytes
+    // S = 64: this wave's 64 * cp.scr_ext bytes, each array lane-interleaved; S = 1: the thread's own bytes
     const int lane = S == 1 ? 0 : (tid & 63);
-    uint8_t *wb = scratch + (S == 1 ? (size_t)tid : (size_t)(tid >> 6) * 64) * (size_t)cp.scratch;
+    uint8_t *wb = scratch + (S == 1 ? (size_t)tid : (size_t)(tid >> 6) * 64) * (size_t)cp.scr_ext;
     ExtCtx<S> X;
     size_t off = 0;
     X.tmp = SP<Reg, S>{reinterpret_cast<Reg *>(wb) + lane};
@@ -1814,12 +2048,19 @@ hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts 
                         const int32_t *sel, int n, const Intv *intv, const int32_t *n_intv, ChainDesc *chains,
                         Seed *seeds, int32_t *n_chains, uint32_t *status, uint8_t *scratch, Counters *ctr)
 {
-    if (sel)   // retry workspaces: a few reads per launch, contiguous per-thread scratch
+    if (sel) {   // retry workspaces: a few reads per launch, contiguous per-thread scratch
         hipLaunchKernelGGL(k_chain<1>, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds,
-                           n_chains, status, scratch, ctr);
-    else
-        hipLaunchKernelGGL(k_chain<64>, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds,
-                           n_chains, status, scratch, ctr);
+                           n_chains, status, scratch, ctr, 0);
+        return hipGetLastError();
+    }
+    // main pass: the reads whose chaining state fits the LDS share (nearly all), then k_chain<64> on the rest
+    // (BSQ_CHAIN_SCRATCH=1: k_chain<64> on every read, for A/B runs)
+    static const bool scratch_only = getenv("BSQ_CHAIN_SCRATCH") && atoi(getenv("BSQ_CHAIN_SCRATCH")) == 1;
+    if (!scratch_only && n > 0)
+        hipLaunchKernelGGL(k_chain_s, dim3((n + 63) / 64), dim3(64), (size_t)CsLds::BYTES, st, ix, o, cp, offs, n, intv,
+                           n_intv, chains, seeds, n_chains, status, ctr);
+    hipLaunchKernelGGL(k_chain<64>, dim3(grid), dim3(256), 0, st, ix, o, cp, offs, sel, n, intv, n_intv, chains, seeds,
+                       n_chains, status, scratch, ctr, scratch_only ? 0 : 1);
     return hipGetLastError();
 }
 

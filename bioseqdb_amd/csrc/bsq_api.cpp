@@ -753,14 +753,22 @@ bool long_reads(int max_len)
     return !(5.5f * std::log((double)max_len) > (double)(0.05f * (float)max_len));
 }
 
+// k_extend's scratch per thread (align_kernels.hip k_extend: tmp regions, their index, seed sort keys, the
+// global eh row of the non-LDS kernel, the introsort stack)
+static int64_t ext_scratch_bytes(const Caps &c)
+{
+    const int64_t ext = (int64_t)c.regs * (int64_t)sizeof(Reg) + ((c.regs * 4 + 15) & ~15) + (int64_t)c.seeds * 8 +
+                        (int64_t)(c.max_len + 2) * 8 + 192 * 4;
+    return (ext + 255) & ~255LL;
+}
+
 int64_t scratch_bytes(const Caps &c, int64_t z_cap)
 {
     int64_t smem = 3LL * (c.max_len + 2) * (int64_t)sizeof(Intv);
     // + the sort / tree-walk stacks kept in this scratch instead of private memory (align_kernels.hip)
     int64_t chain = (int64_t)c.seeds * 24 + (int64_t)c.chains * 40 + (int64_t)(c.chains / 2 + 8) * 84 + 2LL * c.chains * 4 +
                     (192 + 72) * 4;
-    int64_t ext = (int64_t)c.regs * (int64_t)sizeof(Reg) + ((c.regs * 4 + 15) & ~15) + (int64_t)c.seeds * 8 +
-                  (int64_t)(c.max_len + 2) * 8 + 192 * 4;
+    int64_t ext = ext_scratch_bytes(c);
     int64_t r2a = (((int64_t)(c.max_len + 2) * 8 + 63) & ~63LL) + z_cap;
     int64_t m = std::max(std::max(smem, chain), std::max(ext, r2a));
     return (m + 255) & ~255LL;
@@ -772,6 +780,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
 {
     w.cp = cp;
     w.cp.scratch = scratch_bytes(cp, z_cap);
+    w.cp.scr_ext = ext_scratch_bytes(cp);
     w.max_reads = max_reads;
     int threads = std::min<int64_t>(std::max(max_reads, 1), workers);
     w.grid = (threads + 255) / 256;

@@ -92,6 +92,8 @@ struct Caps {
     int32_t regs;        // alignment regions per read
     int32_t cigar;       // CIGAR ops per region
     int64_t scratch;     // bytes of private scratch per worker thread
+    int64_t scr_ext;     // k_extend's stride in that scratch (<= scratch): its own arrays only, so the
+                         // extension's lanes sit closer together than the widest stage's stride puts them
 };
 
 struct Intv { uint64_t x[3]; uint64_t info; };
