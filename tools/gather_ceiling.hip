@@ -182,8 +182,13 @@ int main(int argc, char **argv)
     const int cus = prop.multiProcessorCount;
     uint32_t *sink;
     CHK(hipMalloc(&sink, 4));
-    const uint64_t sizes[2] = {100ull << 20, 3ull << 30};
-    for (uint64_t bytes : sizes) {
+    // GATHER_SWEEP=1: table sizes from 1 MB (L2) to 3 GB, independent gathers and 12 / 16-wave chains only
+    const bool sweep = getenv("GATHER_SWEEP") != nullptr;
+    const uint64_t sizes_all[2] = {100ull << 20, 3ull << 30};
+    const uint64_t sizes_sw[7] = {1ull << 20, 4ull << 20, 16ull << 20, 64ull << 20, 100ull << 20, 256ull << 20, 1ull << 30};
+    const int nsz = sweep ? 7 : 2;
+    for (int zi = 0; zi < nsz; ++zi) {
+        const uint64_t bytes = sweep ? sizes_sw[zi] : sizes_all[zi];
         uint4 *t;
         CHK(hipMalloc(&t, bytes));
         const uint64_t n16 = bytes / 16, nblk = bytes / 32;
@@ -195,7 +200,7 @@ int main(int argc, char **argv)
         float ms = 0;
         // independent gathers: 16 waves per CU of 256-thread blocks, 256 trips x 8 blocks per lane; best of 5
         for (int wpc : {4, 8, 16}) {
-            const int grid = cus * wpc / 4, trips = 256;
+            const int grid = cus * wpc / 4, trips = sweep ? 64 : 256;
             ms = 1e30f;
             for (int rep = 0; rep < 5; ++rep) {
                 float m = 0;
@@ -228,6 +233,7 @@ int main(int argc, char **argv)
                    bytes / 1048576.0, wpc, loads / (ms * 1e-3) / 1e9, loads * 32 / (ms * 1e-3) / 1e9,
                    ms * 1e6 / steps);
         }
+        if (sweep) { CHK(hipFree(t)); continue; }
         sweep_chains<1>(t, nblk, bytes, cus, sink, a, b);
         sweep_chains<2>(t, nblk, bytes, cus, sink, a, b);
         sweep_chains<4>(t, nblk, bytes, cus, sink, a, b);
