@@ -2054,8 +2054,9 @@ hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts 
         return hipGetLastError();
     }
     // main pass: the reads whose chaining state fits the LDS share (nearly all), then k_chain<64> on the rest
-    // (BSQ_CHAIN_SCRATCH=1: k_chain<64> on every read, for A/B runs)
-    static const bool scratch_only = getenv("BSQ_CHAIN_SCRATCH") && atoi(getenv("BSQ_CHAIN_SCRATCH")) == 1;
+    // (BSQ_CHAIN_SCRATCH=1: k_chain<64> on every read, for A/B runs and tests/test_gpu_chain.py)
+    const char *cs_env = getenv("BSQ_CHAIN_SCRATCH");
+    const bool scratch_only = cs_env && atoi(cs_env) == 1;
     if (!scratch_only && n > 0)
         hipLaunchKernelGGL(k_chain_s, dim3((n + 63) / 64), dim3(64), (size_t)CsLds::BYTES, st, ix, o, cp, offs, n, intv,
                            n_intv, chains, seeds, n_chains, status, ctr);
