@@ -331,17 +331,30 @@ def lone_launch(L, idx, opts, codes, offs, n, first_call):
 
 def oracle_index(L, idx, ref_ns):
     """The CPU oracle's index over the same reference rows, its FM tables from the device-built suffix array
-    (the checker for parity and the CPU baseline; test infrastructure, never on the product path)."""
+    (the checker for parity and the CPU baseline; test infrastructure, never on the product path).  The SA is
+    certified twice before the oracle uses it, so the two sides cannot share a wrong one: on the device
+    (bsq_index_certify_sa) and on the host by the oracle itself (range, one primary row, adjacent suffixes
+    strictly increasing).  Both certificates go into SA_CERT (the line's `sa_certificate`)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     oi = O.OracleIndex()
     for buf in ref_ns:
         oi.add_ref(len(oi._keep) + 1, bytes(buf.raw))
+    n_suf, bad = ctypes.c_uint64(), ctypes.c_uint64()
+    t0 = time.perf_counter()
+    N.check(L.bsq_index_certify_sa(idx, ctypes.byref(n_suf), ctypes.byref(bad)))
+    SA_CERT["device"] = {"suffixes": int(n_suf.value), "violations": int(bad.value),
+                         "s": round(time.perf_counter() - t0, 3)}
+    if bad.value:
+        raise SystemExit(f"device SA certificate: {bad.value} violations over {n_suf.value} suffixes")
     eb = ctypes.c_int()
     N.check(L.bsq_index_download(idx))   # host copy of the SA for the oracle's index
     sa = L.bsq_index_sa_data(idx, ctypes.byref(eb))
-    oi.build_from_sa(sa, eb.value)
+    SA_CERT["host"] = oi.build_from_sa(sa, eb.value)
     return O, oi
+
+
+SA_CERT = {}
 
 
 def cpu_baseline(O, oi, oo, codes, offs, n_reads, threads, seeding, seconds, first_call):
@@ -557,6 +570,10 @@ def run_group(args, cfg) -> int:
         result["roofline"] = make_roofline(names[di], di, iso[0], iso[1], r0.n, iso, r0.n, per_read, tr, 1)
         result["kernels"] = {STAGE_KERNEL[names[i]]: {"lone_ms": round(iso[0][i], 3)} for i in range(4)}
     hb.stop()
+    if SA_CERT:
+        result["sa_certificate"] = dict(SA_CERT)
+    # introsort scans stopped by the bound rather than the sentinel over every run in this process (must be 0)
+    result["sort_guard"] = int(L.bsq_sort_guard_total())
     print(json.dumps(result), file=json_out(), flush=True)
     L.bsq_group_free(g)
     L.bsq_index_free(idx)
@@ -1180,6 +1197,10 @@ def main() -> int:
                                      "sample (64 B per occ block of bwt_extend, 8 B per SA value, ceil(bases/4) per "
                                      "reference window, + the packed read)")
     result["roofline"] = make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, reads.n, per_read, tr, S)
+    if SA_CERT:
+        result["sa_certificate"] = dict(SA_CERT)
+    # introsort scans stopped by the bound rather than the sentinel over every run in this process (must be 0)
+    result["sort_guard"] = int(L.bsq_sort_guard_total())
     hb.stop()
     if rank == 0:
         print(json.dumps(result), file=json_out(), flush=True)

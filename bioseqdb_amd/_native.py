@@ -108,6 +108,8 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                            ctypes.POINTER(ctypes.c_int64)]),
     "bsq_batch_retried": (ctypes.c_int64, [_P]),
+    "bsq_batch_sort_guard": (ctypes.c_int64, [_P]),
+    "bsq_sort_guard_total": (ctypes.c_int64, []),
     "bsq_batch_copy_records": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "bsq_index_build_device": (ctypes.c_int, [_P, ctypes.c_int]),
     "bsq_batch_run_many": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(Opts),
@@ -117,6 +119,7 @@ SIGNATURES = {
     "bsq_batch_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "bsq_index_download": (ctypes.c_int, [_P]),
     "bsq_index_build_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)]),
+    "bsq_index_certify_sa": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "bsq_nuclseq_encode_batch": (ctypes.c_int, [ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int,
                                                 ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "bsq_nuclseq_decode_batch": (ctypes.c_int, [ctypes.c_int, _P, ctypes.c_int64, ctypes.POINTER(_P),

@@ -243,6 +243,16 @@ class BwaIndex:
         self._built = True
         self._uploaded = True
 
+    def certify_sa(self) -> dict:
+        """The device certificate of the suffix array in HBM (bsq_index_certify_sa): range, every position
+        once, adjacent suffixes strictly increasing; violations == 0 proves it is the SA of T$."""
+        import time
+        n, bad = ctypes.c_uint64(), ctypes.c_uint64()
+        t0 = time.perf_counter()
+        check(lib().bsq_index_certify_sa(self._h, ctypes.byref(n), ctypes.byref(bad)))
+        return {"suffixes": int(n.value), "violations": int(bad.value),
+                "device_s": round(time.perf_counter() - t0, 3)}
+
     def upload(self) -> None:
         if not self._uploaded and self.l_pac > 0:
             check(lib().bsq_index_upload(self._h, self.device))

@@ -300,13 +300,18 @@ DEV void ks_combsort(A a, int n, LT lt)
 
 // stk: 3 x 64 ints of the thread's global scratch (the partition stack, touched only by partitions of more
 // than 16 elements): a private array here would give every wave of the kernel a scratch segment
+// Returns the number of partition scans that reached the bound `i == t` while `lt(a[t], rp)` still held, i.e.
+// scans that klib's sentinel would NOT have stopped (the runaway the round-2 hang would need).  With strict
+// comparators the sentinel a[t] == rp is never swapped, so this is 0; the kernels add it to Counters::sort_guard
+// and the tests and bench assert 0 (a non-zero count names the read to start a root cause from).
 template <class A, class LT, class S>
-DEV void ks_introsort(A a, int n, LT lt, S stk)
+DEV int ks_introsort(A a, int n, LT lt, S stk)
 {
-    if (n < 1) return;
+    int guard = 0;
+    if (n < 1) return 0;
     if (n == 2) {
         if (lt(a[1], a[0])) { int t = a[0]; a[0] = a[1]; a[1] = t; }
-        return;
+        return 0;
     }
     int d;
     for (d = 2; (1ul << d) < (unsigned long)n; ++d);
@@ -336,6 +341,7 @@ DEV void ks_introsort(A a, int n, LT lt, S stk)
                 do ++i; while (lt(a[i], rp));
 #else
                 do ++i; while (i < t && lt(a[i], rp));
+                if (i == t && lt(a[t], rp)) ++guard;   // stopped by the bound, not by the sentinel
 #endif
                 do --j; while (i <= j && lt(rp, a[j]));
                 if (j <= i) break;
@@ -350,7 +356,7 @@ DEV void ks_introsort(A a, int n, LT lt, S stk)
                 t = i - s > 16 ? i - 1 : s;
             }
         } else {
-            if (top == 0) { ks_insertsort(a, n, lt); return; }
+            if (top == 0) { ks_insertsort(a, n, lt); return guard; }
             --top; s = stk_l[top]; t = stk_r[top]; d = stk_d[top];
         }
     }
@@ -523,6 +529,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
     const int nthr = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t nsa = 0;
+    int guard = 0;
     // S = 64: this wave's 64 * cp.scratch bytes, each array lane-interleaved (SP); the workspace holds whole
     // waves.  S = 1 (retry workspaces): the thread's own cp.scratch bytes, arrays contiguous.
     const int lane = S == 1 ? 0 : (tid & 63);
@@ -617,7 +624,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         }
         if (n_chn > 0) {
             const SP<ChainNode, S> ch = C.ch;
-            ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; }, stk);
+            guard += ks_introsort(ord, n_chn, [ch](int a, int b) { return ch[a].w > ch[b].w; }, stk);
             ch[ord[0]].kept = 3;
             int nk = 0;
             kept_list[nk++] = 0;
@@ -675,6 +682,7 @@ __global__ void __launch_bounds__(256) k_chain(DIndex ix, DOpts o, Caps cp, cons
         }
     }
     wave_add(&ctr[STG_CHAIN].sa_values, nsa);
+    wave_add(&ctr[STG_CHAIN].sort_guard, (unsigned long long)guard);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -747,6 +755,7 @@ __global__ void __launch_bounds__(64) k_chain_s(DIndex ix, DOpts o, Caps cp, con
     const CsLds L{(int)threadIdx.x};
     const int NS = cp.seeds < CS_NS ? cp.seeds : CS_NS, NC = cp.chains < CS_NC ? cp.chains : CS_NC;
     uint64_t nsa = 0;
+    int guard = 0;
     for (int li = tid; li < n; li += nthr) {
         n_chains[li] = 0;
         if (status[li]) continue;
@@ -853,7 +862,7 @@ __global__ void __launch_bounds__(64) k_chain_s(DIndex ix, DOpts o, Caps cp, con
             if (w >= o.min_chain_weight) ord[n_chn++] = (uint8_t)ci;
         }
         if (n_chn > 0) {
-            ks_introsort(ord, n_chn, [L](int a, int b) { return L.cw(a) > L.cw(b); }, SP<int>{nullptr});
+            guard += ks_introsort(ord, n_chn, [L](int a, int b) { return L.cw(a) > L.cw(b); }, SP<int>{nullptr});
             L.ck(ord[0]) = 3;
             int nkl = 0;
             kept_list[nkl++] = 0;
@@ -908,6 +917,7 @@ __global__ void __launch_bounds__(64) k_chain_s(DIndex ix, DOpts o, Caps cp, con
         }
     }
     wave_add(&ctr[STG_CHAIN].sa_values, nsa);
+    wave_add(&ctr[STG_CHAIN].sort_guard, (unsigned long long)guard);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1451,6 +1461,7 @@ struct ExtCtx {
     SP<int2, S> eh;
     SP<int, S> stk;        // introsort stack (192 ints)
     bool ovf;
+    int guard = 0;         // ks_introsort scans stopped by the bound (Counters::sort_guard)
 };
 
 struct QMakeG {   // query accessors over the read in global memory
@@ -1692,7 +1703,7 @@ DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, Ext
     if (n <= 1) return n;
     Reg *a = X.av;
     for (i = 0; i < n; ++i) X.idx[i] = i;
-    ks_introsort(X.idx, n, [a](int x, int y) { return a[x].re < a[y].re; }, X.stk);
+    X.guard += ks_introsort(X.idx, n, [a](int x, int y) { return a[x].re < a[y].re; }, X.stk);
     permute(X, n);
     for (i = 0; i < n; ++i) a[i].n_comp = 1;
     for (i = 1; i < n; ++i) {
@@ -1726,7 +1737,7 @@ DEV int sort_dedup_patch(const DIndex &ix, const DOpts &o, const uint8_t *q, Ext
         if (a[i].qe > a[i].qb) { if (m != i) a[m++] = a[i]; else ++m; }
     n = m;
     for (i = 0; i < n; ++i) X.idx[i] = i;
-    ks_introsort(X.idx, n, [a](int x, int y) {
+    X.guard += ks_introsort(X.idx, n, [a](int x, int y) {
         return a[x].score > a[y].score || (a[x].score == a[y].score && (a[x].rb < a[y].rb || (a[x].rb == a[y].rb && a[x].qb < a[y].qb)));
     }, X.stk);
     permute(X, n);
@@ -1747,7 +1758,7 @@ DEV void mark_primary_se(const DOpts &o, ExtCtx<S> &X, int64_t id)
         a[i].sub = 0; a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i));
         X.idx[i] = i;
     }
-    ks_introsort(X.idx, n, [a](int x, int y) {
+    X.guard += ks_introsort(X.idx, n, [a](int x, int y) {
         return a[x].score > a[y].score || (a[x].score == a[y].score && a[x].hash < a[y].hash);
     }, X.stk);
     permute(X, n);
@@ -1849,6 +1860,7 @@ __global__ void __launch_bounds__(LDS ? 64 : 256) k_extend(DIndex ix, DOpts o, C
     }
     wave_add(&ctr[STG_EXTEND].dp_cells, cells);
     wave_add(&ctr[STG_EXTEND].ref_bases, bases);
+    wave_add(&ctr[STG_EXTEND].sort_guard, (unsigned long long)X.guard);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -10,6 +10,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -77,6 +78,7 @@ hipError_t launch_col_write(hipStream_t, const RenderView &, const int64_t *, co
                             const int64_t *, const uint8_t *, uint8_t *);
 hipError_t gpu_build_index(const uint8_t *, int64_t, bool, hipStream_t, void **, OccBlock **, uint64_t *, uint64_t[5],
                            uint64_t *, int *, uint64_t *, std::string &);
+hipError_t gpu_certify_sa(const uint8_t *, int64_t, bool, const void *, hipStream_t, uint64_t *);
 hipError_t launch_occ32(hipStream_t, const OccBlock *, uint64_t, OccBlock32 *, int);
 hipError_t launch_intv_counts(hipStream_t, int, const int32_t *, const uint32_t *, int64_t *);
 hipError_t launch_intv_pack(hipStream_t, int, int, const Intv *, const int32_t *, const uint32_t *, const int64_t *,
@@ -107,6 +109,7 @@ struct Range {
 };
 
 static thread_local std::string g_err;
+static std::atomic<int64_t> g_sort_guard{0};   // bsq_sort_guard_total: every batch run in the process
 static void set_err(const char *fmt, ...)
 {
     char buf[512];
@@ -555,6 +558,25 @@ extern "C" int bsq_index_build_device(bsq_index *idx, int device)
     return BSQ_OK;
 }
 
+extern "C" int bsq_index_certify_sa(const bsq_index *idx, uint64_t *suffixes, uint64_t *violations)
+{
+    Range rg("bsq_index_certify_sa");
+    if (!idx || !idx->h.built || !idx->h.dev) { set_err("index not on a device"); return BSQ_E_INVALID; }
+    const HostIndex &h = idx->h;
+    if (suffixes) *suffixes = h.seq_len ? h.seq_len + 1 : 0;
+    if (violations) *violations = 0;
+    if (h.seq_len == 0) return BSQ_OK;
+    HIPCHK(hipSetDevice(h.dev->device));
+    uint64_t bad = 0;
+    const hipError_t e = gpu_certify_sa(h.dev->pac, h.l_pac, meta_of(h).wide != 0, h.dev->sa, nullptr, &bad);
+    if (e != hipSuccess) {
+        set_err("SA certificate: %s", hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? BSQ_E_NOMEM : BSQ_E_HIP;
+    }
+    if (violations) *violations = bad;
+    return BSQ_OK;
+}
+
 extern "C" int bsq_index_build_stats(const bsq_index *idx, int *rounds, uint64_t *tied)
 {
     if (!idx || !idx->h.dev_built) { set_err("not a device-built index"); return BSQ_E_INVALID; }
@@ -910,6 +932,7 @@ struct bsq_batch {
     float stage_ms[STG_N]{};
     double stage_bytes[STG_N]{};
     double stage_work[STG_N]{};
+    int64_t sort_guard = 0;   // ks_introsort scans stopped by the bound over every run of this batch (must stay 0)
     int64_t retried = 0;
     bool dev_whole = false;   // d_out / d_out_cig hold the whole last run's view (one chunk, no retried read)
     // record route (bsq_batch_set_record_route): the packed records cross to relay_dev's HBM by peer DMA (xGMI between
@@ -988,7 +1011,9 @@ extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_b
     for (auto &e : b->ev) HIPCHK(hipEventCreate(&e));
     const size_t R = (size_t)std::max(max_reads, 1);
     // whole 16-B words plus one: the reg2aln query stream loads the aligned word holding a read's last base
-    HIPCHK(hipMalloc(&b->codes, (size_t)((std::max<int64_t>(max_bases, 1) + 15) / 16 * 16 + 16)));
+    // 32 bytes of padding past the last 16-base word: render_gpu.hip's codes16 loads 8 bytes from an aligned
+    // address up to 12 bytes beyond a word's start, i.e. up to 19 bytes past the last base
+    HIPCHK(hipMalloc(&b->codes, (size_t)((std::max<int64_t>(max_bases, 1) + 15) / 16 * 16 + 32)));
     HIPCHK(hipMalloc(&b->offs, (R + 1) * 8));
     HIPCHK(hipMalloc(&b->ids, R * 8));
     HIPCHK(hipMalloc(&b->ctr, sizeof(Counters) * STG_N));
@@ -1659,6 +1684,11 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
         b->stage_bytes[STG_D2H] = b->stage_bytes[STG_PACK];
         for (int s = 0; s < STG_N; ++s) b->stage_work[s] = (double)c[s].dp_cells;
         b->stage_work[STG_SMEM] = (double)c[STG_SMEM].kmer_hits + (double)c[STG_SMEM].occ_blocks / 2.0;
+        {
+            const int64_t g = (int64_t)(c[STG_CHAIN].sort_guard + c[STG_EXTEND].sort_guard);
+            b->sort_guard += g;
+            if (g) g_sort_guard.fetch_add(g);
+        }
     } else {
         for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     }
@@ -2051,6 +2081,9 @@ extern "C" int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max)
     for (int s = 0; s < STG_N && s < max; ++s) bytes[s] = b->stage_bytes[s];
     return STG_N;
 }
+
+extern "C" int64_t bsq_batch_sort_guard(const bsq_batch *b) { return b ? b->sort_guard : -1; }
+extern "C" int64_t bsq_sort_guard_total(void) { return g_sort_guard.load(); }
 
 extern "C" int bsq_batch_stage_work(const bsq_batch *b, double *work, int max)
 {

@@ -124,7 +124,8 @@ struct Counters {
     unsigned long long dp_cells;     // DP cells evaluated (secondary figure)
     unsigned long long overflow;     // reads flagged for the retry pass
     unsigned long long kmer_hits;    // 16-B k-mer interval table reads (in place of a bwt_extend)
-    unsigned long long pad[2];
+    unsigned long long sort_guard;   // introsort partition scans stopped by the i < t bound, not the sentinel (must be 0)
+    unsigned long long pad;
 };
 
 }  // namespace bsq

@@ -302,6 +302,31 @@ struct Bufs {   // frees whatever is still allocated on every exit path
 
 #define GCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return e_; } } while (0)
 
+// The SA certificate over a suffix array in HBM: range, every position once (a bitmap of N bits) and
+// adjacent suffixes strictly increasing; *bad = the number of violations (0 = it is the SA of T$).
+template <typename P>
+hipError_t certify_impl(const uint8_t *d_pac, int64_t l_pac, const P *sa, hipStream_t st, uint64_t *bad)
+{
+    const uint64_t N = ((uint64_t)l_pac << 1) + 1;
+    uint32_t *seen = nullptr;
+    unsigned long long *d_bad = nullptr;
+    hipError_t e = hipMalloc(&seen, (N + 31) / 32 * 4);
+    if (e == hipSuccess) e = hipMalloc(&d_bad, 8);
+    if (e == hipSuccess) e = hipMemsetAsync(seen, 0, (N + 31) / 32 * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 8, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_verify_sa<P>, grid_of(N), dim3(256), 0, st, d_pac, l_pac, N, sa, seen, d_bad);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_bad, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFree(seen);
+    hipFree(d_bad);
+    *bad = h;
+    return e;
+}
+
 template <typename P>
 hipError_t build_impl(const uint8_t *d_pac, int64_t l_pac, hipStream_t st, void **sa_out, OccBlock **occ_out,
                       uint64_t *primary_out, uint64_t L2[5], uint64_t *nblk_out, int *rounds_out, uint64_t *tied_out,
@@ -557,18 +582,11 @@ hipError_t build_impl(const uint8_t *d_pac, int64_t l_pac, hipStream_t st, void 
     L2[0] = 0;
     for (int c = 0; c < 4; ++c) L2[c + 1] = L2[c] + tot[c];
     if (check) {
-        uint32_t *seen;
-        GCHK(B.alloc(seen, (N + 31) / 32));
-        GCHK(hipMemsetAsync(seen, 0, (N + 31) / 32 * 4, st));
-        unsigned long long *d_bad = reinterpret_cast<unsigned long long *>(d_sel), bad = 0;
-        GCHK(hipMemsetAsync(d_bad, 0, 8, st));
-        hipLaunchKernelGGL(k_verify_sa<P>, grid_of(N), dim3(256), 0, st, d_pac, l_pac, N, (const P *)sa, seen, d_bad);
-        GCHK(hipGetLastError());
-        GCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, st));
-        GCHK(hipStreamSynchronize(st));
-        fprintf(stderr, "[bsq index] SA certificate over %llu suffixes: %llu violations\n", (unsigned long long)N, bad);
+        uint64_t bad = 0;
+        GCHK(certify_impl<P>(d_pac, l_pac, (const P *)sa, st, &bad));
+        fprintf(stderr, "[bsq index] SA certificate over %llu suffixes: %llu violations\n", (unsigned long long)N,
+                (unsigned long long)bad);
         if (bad) { err = "suffix array certificate failed"; return hipErrorUnknown; }
-        B.release(seen);
     }
     B.keep(sa); B.keep(occ);
     *sa_out = sa;
@@ -589,6 +607,14 @@ hipError_t gpu_build_index(const uint8_t *d_pac, int64_t l_pac, bool wide, hipSt
 {
     if (wide) return build_impl<uint64_t>(d_pac, l_pac, st, sa, occ, primary, L2, nblk, rounds, tied, err);
     return build_impl<uint32_t>(d_pac, l_pac, st, sa, occ, primary, L2, nblk, rounds, tied, err);
+}
+
+// The certificate of a suffix array already in HBM (bsq_index_certify_sa): *violations = 0 iff sa is the SA of T$.
+hipError_t gpu_certify_sa(const uint8_t *d_pac, int64_t l_pac, bool wide, const void *sa, hipStream_t st,
+                          uint64_t *violations)
+{
+    if (wide) return certify_impl<uint64_t>(d_pac, l_pac, (const uint64_t *)sa, st, violations);
+    return certify_impl<uint32_t>(d_pac, l_pac, (const uint32_t *)sa, st, violations);
 }
 
 }  // namespace bsq

@@ -129,6 +129,10 @@ int bsq_index_build_device(bsq_index *idx, int device);
 int bsq_index_download(bsq_index *idx);
 /* Prefix-doubling rounds of the last device build and the suffixes still tied after its first sort. */
 int bsq_index_build_stats(const bsq_index *idx, int *rounds, uint64_t *tied);
+/* Certificate of the suffix array in HBM (either build): every value in range, every position once, adjacent
+ * suffixes of T$ strictly increasing.  *violations == 0 proves it is the unique SA that libbwa's bwt_cal_sa
+ * samples (bioseqdb/bwa.cpp:107-128), so the BWT and occ derived from it are libbwa's.  *suffixes = seq_len+1. */
+int bsq_index_certify_sa(const bsq_index *idx, uint64_t *suffixes, uint64_t *violations);
 int64_t bsq_index_l_pac(const bsq_index *idx);
 int64_t bsq_index_seq_len(const bsq_index *idx);
 int64_t bsq_index_primary(const bsq_index *idx);
@@ -345,6 +349,12 @@ int bsq_batch_stage_bytes(const bsq_batch *b, double *bytes, int max);
 int bsq_batch_stage_work(const bsq_batch *b, double *work, int max);
 /* Number of reads of the last run that needed the large-capacity retry pass. */
 int64_t bsq_batch_retried(const bsq_batch *b);
+/* Partition scans of klib's introsort (mem_chain_flt, mem_sort_dedup_patch, mem_mark_primary_se) that the kernels'
+ * `i < t` bound stopped where klib's sentinel would not have -- summed over every run of this batch.  Always 0
+ * for a correct sort (the sentinel is never swapped); the tests and bench.py assert it.  -1 for NULL. */
+int64_t bsq_batch_sort_guard(const bsq_batch *b);
+/* The same count over every batch run in this process (pipelines, one-shot calls and groups included). */
+int64_t bsq_sort_guard_total(void);
 
 #ifdef __cplusplus
 }

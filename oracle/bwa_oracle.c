@@ -394,6 +394,44 @@ static void run_jobs(bwt_job *jobs, int nt, void *(*fn)(void *))
     for (int t = 1; t < nt; ++t) pthread_join(th[t], NULL);
 }
 
+/* Suffix a of T$ (T[n] = $, smaller than every base) strictly below suffix b?  Eight characters per step:
+ * T holds one base 0..3 per byte, so a big-endian word compare is the lexicographic one. */
+static int suffix_less(const uint8_t *T, uint64_t n, uint64_t a, uint64_t b)
+{
+    while (a + 8 <= n && b + 8 <= n) {
+        uint64_t x, y;
+        memcpy(&x, T + a, 8); memcpy(&y, T + b, 8);
+        if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y);
+        a += 8; b += 8;
+    }
+    for (;; ++a, ++b) {
+        if (a == n || b == n) return a == n && b != n;   /* $ ends the shorter suffix; a == b is no order */
+        if (T[a] != T[b]) return T[a] < T[b];
+    }
+}
+
+/* The host certificate of an SA handed in from outside (orc_index_build_from_sa): rows [lo, hi) must hold
+ * strictly increasing suffixes (row hi-1 against row hi too).  With every value already checked to lie in
+ * [0, n] (bwt_find_primary), n+1 strictly increasing suffixes are n+1 distinct positions of n+1: the array
+ * is a permutation, hence THE suffix array of T$, so the BWT and occ built from it are libbwa's. */
+static void *sa_check_order(void *a)
+{
+    bwt_job *j = a;
+    j->bad = 0;
+    if (j->lo >= j->hi) return NULL;
+    uint64_t prev = sa_at(j, j->lo);
+    for (uint64_t i = j->lo + 1; i <= j->hi && i <= j->n; ++i) {
+        if (i + 32 <= j->n) __builtin_prefetch(j->T + sa_at(j, i + 32));   /* one random line per row */
+        const uint64_t s = sa_at(j, i);
+        j->bad += !suffix_less(j->T, j->n, prev, s);
+        prev = s;
+    }
+    return NULL;
+}
+
+static uint64_t orc_sa_violations_last;
+uint64_t orc_sa_violations(void) { return orc_sa_violations_last; }
+
 static int finish_bwt(orc_index *idx, const uint8_t *T, uint64_t n, const int64_t *sa64, const void *sa_ext, int sa_bytes)
 {
     uint64_t i, c[4];
@@ -414,6 +452,14 @@ static int finish_bwt(orc_index *idx, const uint8_t *T, uint64_t n, const int64_
         if (jobs[t].found != (uint64_t)-1) { primary = jobs[t].found; ++nfound; }
     }
     if (nfound != 1) return -1;
+    if (!sa64) {   /* an SA from outside (the GPU build): certify order, which with the range implies permutation */
+        for (int t = 0; t < nt; ++t) { jobs[t].lo = (n + 1) * (uint64_t)t / nt; jobs[t].hi = (n + 1) * (uint64_t)(t + 1) / nt; }
+        run_jobs(jobs, nt, sa_check_order);
+        uint64_t bad = 0;
+        for (int t = 0; t < nt; ++t) bad += jobs[t].bad;
+        orc_sa_violations_last = bad;
+        if (bad) return -2;
+    }
     idx->primary = primary;
     uint32_t *raw = calloc(idx->bwt_size + 1, 4);
     for (int t = 0; t < nt; ++t) {

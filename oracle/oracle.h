@@ -50,9 +50,14 @@ void orc_index_add_ref(orc_index *idx, int64_t id, const uint8_t *nuclseq);
 /* Builds BWT/occ/SA with the oracle's own suffix sort. Returns 0 on success. */
 int orc_index_build(orc_index *idx);
 /* Builds BWT/occ/SA from an externally supplied suffix array of T$ (n+1 entries; sa_bytes = 4 or 8).
- * Used only by bench.py's cpu_baseline leg to skip the O(n log n) oracle sort on 100 Mbp inputs.
- * The SA is verified to be a permutation with B[] derivable; returns 0 on success. */
+ * Used by the BASELINE-size parity fixtures and bench.py's cpu_baseline leg to skip the oracle's own
+ * O(n log n) sort on 100 Mbp / 3 Gbp inputs.  The SA is certified on the host first (16 threads): every
+ * value in [0, n], exactly one row 0, and adjacent rows' suffixes of T$ strictly increasing -- which
+ * makes it a permutation and so the unique suffix array.  Returns 0 on success, -1 for a range/primary
+ * fault, -2 for order violations (their count: orc_sa_violations). */
 int orc_index_build_from_sa(orc_index *idx, const void *sa, int sa_bytes);
+/* Order violations found by the last orc_index_build_from_sa (0 after a certified build). */
+uint64_t orc_sa_violations(void);
 int64_t orc_index_l_pac(const orc_index *idx);
 int64_t orc_index_seq_len(const orc_index *idx);
 int64_t orc_index_primary(const orc_index *idx);

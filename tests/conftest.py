@@ -25,6 +25,19 @@ def _ensure_built():
 _ensure_built()
 
 
+@pytest.fixture(autouse=True)
+def _introsort_guard_stays_zero(request):
+    """every GPU test ends with bsq_sort_guard_total() == 0 -- no introsort partition scan in
+    k_chain / k_chain_s / k_extend was stopped by the `i < t` bound instead of klib's sentinel (the round-2
+    hang's would-be runaway).  A non-zero count fails the test that produced it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    from bioseqdb_amd._native import lib
+    g = lib().bsq_sort_guard_total()
+    assert g == 0, f"{g} introsort scans stopped by the bound, not the sentinel"
+
+
 @pytest.fixture(scope="session")
 def gpu_available():
     from bioseqdb_amd._native import lib

@@ -1,7 +1,9 @@
 """Regenerates the committed golden fixtures (inputs + oracle outputs).  Run from the repo root:
     python tests/golden/make_golden.py
-The fixtures pin the oracle against regressions (tests/test_golden.py) and give the GPU path a
-fixed input/output set (tests/test_gpu_golden.py).  Inputs are stored as text so they do not depend
+The fixtures pin the oracle against regressions (tests/test_golden.py::test_oracle_reproduces_golden) and
+give the GPU path a fixed input/output set (tests/test_golden.py::test_gpu_matches_golden, marked gpu).  The
+expected outputs are the oracle's own, so they pin the oracle against itself and the GPU against the oracle,
+not either against libbwa (absent here).  Inputs are stored as text so they do not depend
 on the generator's numpy version."""
 import json
 import os

@@ -49,6 +49,7 @@ def lib() -> ctypes.CDLL:
             "orc_index_add_ref": (None, [P, ctypes.c_int64, P]),
             "orc_index_build": (ctypes.c_int, [P]),
             "orc_index_build_from_sa": (ctypes.c_int, [P, P, ctypes.c_int]),
+            "orc_sa_violations": (ctypes.c_uint64, []),
             "orc_index_l_pac": (ctypes.c_int64, [P]),
             "orc_index_seq_len": (ctypes.c_int64, [P]),
             "orc_index_primary": (ctypes.c_int64, [P]),
@@ -128,8 +129,16 @@ class OracleIndex:
     def build(self) -> None:
         assert lib().orc_index_build(self.h) == 0
 
-    def build_from_sa(self, sa_ptr: int, elem_bytes: int) -> None:
-        assert lib().orc_index_build_from_sa(self.h, sa_ptr, elem_bytes) == 0
+    def build_from_sa(self, sa_ptr: int, elem_bytes: int) -> dict:
+        """FM tables from an outside suffix array, certified on the host first (range, one primary row,
+        adjacent suffixes strictly increasing => the unique SA of T$); returns the certificate."""
+        import time
+        t0 = time.perf_counter()
+        rc = lib().orc_index_build_from_sa(self.h, sa_ptr, elem_bytes)
+        cert = {"suffixes": self.seq_len + 1 if rc == 0 else None, "violations": int(lib().orc_sa_violations()),
+                "rc": rc, "host_s": round(time.perf_counter() - t0, 2)}
+        assert rc == 0, f"suffix array rejected by the host certificate: {cert}"
+        return cert
 
     @property
     def l_pac(self) -> int:

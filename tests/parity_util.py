@@ -26,6 +26,35 @@ def build_pair(ref_texts, ids=None, opts=None):
     return pi, oi
 
 
+def oracle_from_device_sa(pi, oi, label):
+    """The oracle's FM tables for a device-built index at the BASELINE sizes, where the oracle's own suffix sort
+    is too slow: from the GPU's suffix array, but only after two independent certificates -- the device one
+    (bsq_index_certify_sa: range, every position once, adjacent suffixes increasing) and the oracle's host one
+    inside orc_index_build_from_sa (range, one primary row, adjacent suffixes strictly increasing => a
+    permutation).  Either proves the SA is the unique SA of T$, so a wrong SA cannot reach both sides of the
+    parity check.  Both certificates are appended to gpurun_out/sa_certificates.jsonl (kept under profiles/)."""
+    import ctypes
+    import json
+    import os
+    from bioseqdb_amd import _native as N
+    L = N.lib()
+    dev = pi.certify_sa()
+    assert dev["violations"] == 0 and dev["suffixes"] == L.bsq_index_seq_len(pi.handle) + 1, dev
+    N.check(L.bsq_index_download(pi.handle))
+    eb = ctypes.c_int()
+    sa = L.bsq_index_sa_data(pi.handle, ctypes.byref(eb))
+    host = oi.build_from_sa(sa, eb.value)
+    assert host["violations"] == 0 and host["suffixes"] == dev["suffixes"], host
+    assert oi.primary == L.bsq_index_primary(pi.handle)
+    rec = {"config": label, "sa_elem_bytes": eb.value, "device": dev, "host": host}
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "sa_certificates.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
+    print(f"[sa certificate] {label}: {json.dumps(rec)}", flush=True)
+    return rec
+
+
 def compare(pi, oi, read_texts, first_call=0, opts=None):
     """Returns (n_rows_checked, mismatches[list of (read, field, gpu, oracle)])."""
     o = pi.options if opts is None else opts

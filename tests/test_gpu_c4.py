@@ -3,8 +3,11 @@
 At 2 x 3e9 = 6e9 suffixes the index takes the 64-bit-row path for real (u64 suffix array, u64 SMEM lists,
 k-mer table at K = 11, occ blocks of a 3 GB BWT outside the Infinity Cache).  The reference itself cannot
 build this index at all (is_bwt takes an int length: bioseqdb/bwa.cpp:10,47; rows are capped at
-INT32_MAX/4 bases: extension.cpp:50), so the oracle is the only check: its FM tables are re-derived (and
-verified) from the GPU-built suffix array, which is unique, so nothing else the GPU computes is reused.
+INT32_MAX/4 bases: extension.cpp:50), so the oracle is the only check.  Its FM tables are derived on the host
+from the GPU-built suffix array once that SA has passed two certificates, each a proof that it is the unique SA
+of T$ over all 6e9 suffixes: the device one (bsq_index_certify_sa: range, every position once, adjacent suffixes
+increasing) and the oracle's own host check (range, one primary row, adjacent suffixes strictly increasing;
+orc_index_build_from_sa).  A mis-sorted SA therefore cannot reach both sides (parity_util.oracle_from_device_sa).
 
 * all 14 bwa_result columns of 20k reads (bsq_align_batch + bsq_render_tsv, the path of
   BwaIndex::align_sequence, bwa.cpp:141-181) against the oracle's rows;
@@ -24,7 +27,7 @@ import pytest
 import oracle_py as O
 from bioseqdb_amd import BwaIndex, NucleotideSequence, effective_opts, loader, synth
 from bioseqdb_amd import _native as N
-from parity_util import _oracle_batch_tsv, compare_batch, compare_tsv
+from parity_util import _oracle_batch_tsv, compare_batch, compare_tsv, oracle_from_device_sa
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -52,12 +55,8 @@ def c4_pair():
     pi.build_on_device()
     L = N.lib()
     assert L.bsq_index_seq_len(pi.handle) == 6_000_000_000 > 2 ** 32
-    N.check(L.bsq_index_download(pi.handle))
-    eb = ctypes.c_int()
-    sa = L.bsq_index_sa_data(pi.handle, ctypes.byref(eb))
-    assert eb.value == 8   # 64-bit suffix array
-    oi.build_from_sa(sa, eb.value)
-    assert oi.primary == L.bsq_index_primary(pi.handle)
+    cert = oracle_from_device_sa(pi, oi, "C4 3 Gbp")
+    assert cert["sa_elem_bytes"] == 8   # 64-bit suffix array
     pi.options = effective_opts(None, 24)
     yield ref, pi, oi
     del pi, oi

@@ -2,8 +2,11 @@
 
 * C3 (configs[2]): 100 Mbp synthetic reference, 20k x 150 bp reads, all 14 bwa_result columns of the
   GPU path (bsq_align_batch + bsq_render_tsv) against the CPU oracle, row by row (ref_subseq skipped on
-  reverse rows, Q7).  The oracle's FM tables come from the GPU-built suffix array (orc_index_build_from_sa
-  re-derives and verifies BWT/occ/L2 from it), which is unique, so nothing the GPU computes is reused.
+  reverse rows, Q7).  The oracle's FM tables (BWT, occ, L2, sampled SA) are derived on the host from the
+  GPU-built suffix array, after the SA has passed two certificates that each prove it is the unique SA of T$:
+  the device one (bsq_index_certify_sa) and the oracle's own host check (range, one primary row, adjacent
+  suffixes strictly increasing; orc_index_build_from_sa).  The oracle's own suffix sort is too slow at 2e8
+  suffixes; the certificates are what keeps a mis-sorted SA from reaching both sides (parity_util).
 * C2 (configs[1]): seeding only on the same index, bsq_batch_seed intervals against orc_collect_intv.
 * The option matrix: non-default bwa_opts() values, with the Q1 field swap and the Q2 scoring matrix
   that keeps a=1/b=4 while opt->a/opt->b change (bioseqdb/bwa.cpp:80, extension.cpp:220-231).
@@ -16,7 +19,7 @@ import pytest
 import oracle_py as O
 from bioseqdb_amd import BwaIndex, NucleotideSequence, bwa_opts, effective_opts, synth
 from bioseqdb_amd import _native as N
-from parity_util import build_pair, compare_batch
+from parity_util import build_pair, compare_batch, oracle_from_device_sa
 
 pytestmark = pytest.mark.gpu
 
@@ -39,11 +42,7 @@ def c3_pair():
         pi.add_ref_sequence(i + 1, ns)
         oi.add_ref(i + 1, on.raw)
     pi.build_on_device()
-    N.check(N.lib().bsq_index_download(pi.handle))
-    eb = ctypes.c_int()
-    sa = N.lib().bsq_index_sa_data(pi.handle, ctypes.byref(eb))
-    oi.build_from_sa(sa, eb.value)
-    assert oi.primary == N.lib().bsq_index_primary(pi.handle)
+    oracle_from_device_sa(pi, oi, "C3 100 Mbp")
     pi.options = effective_opts(None, len(ref.rows))
     return ref, pi, oi
 

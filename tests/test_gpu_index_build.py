@@ -135,3 +135,46 @@ def test_replicate_from_device_build():
     import gc
     gc.collect()
     del bufs
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_sa_certificate_detects_corruption(monkeypatch, wide):
+    """bsq_index_certify_sa (the device certificate the C3/C4 parity fixtures and bench's oracle leg run): 0
+    violations for the device build and for a host build uploaded, and > 0 once two SA rows are swapped or one
+    row duplicated in HBM (the SA table lives in caller-owned torch buffers via bsq_index_upload_into)."""
+    import gc
+    import torch
+    if wide:
+        monkeypatch.setenv("BSQ_FORCE_WIDE", "1")
+    L = N.lib()
+    ref = synth.make_reference(150_000, n_rows=2, n_run_every=60_000, n_run_len=100)
+    host, dev = _pair([t.decode() for t in ref.texts()])
+    host.upload()
+    for x in (host, dev):
+        c = x.certify_sa()
+        assert c["violations"] == 0 and c["suffixes"] == L.bsq_index_seq_len(x.handle) + 1, c
+    sizes = (ctypes.c_uint64 * N.N_TABLES)()
+    mb = ctypes.c_uint64()
+    N.check(L.bsq_index_layout(dev.handle, sizes, None, ctypes.byref(mb)))
+    bufs = [torch.empty(int(b), dtype=torch.uint8, device="cuda:0") if b else None for b in sizes]
+    tabs = (N.Table * N.N_TABLES)(*[N.Table(t.data_ptr() if t is not None else None, int(b)) for t, b in zip(bufs, sizes)])
+    N.check(L.bsq_index_upload_into(dev.handle, 0, tabs, N.N_TABLES))
+    sa = bufs[2].view(torch.int64 if wide else torch.int32)   # T_SA
+    assert dev.certify_sa()["violations"] == 0
+    good = sa.clone()
+    n = sa.numel()
+    for i in (1, n // 2, n - 2):
+        sa.copy_(good)
+        sa[i], sa[i + 1] = good[i + 1].item(), good[i].item()
+        torch.cuda.synchronize()
+        assert dev.certify_sa()["violations"] >= 1, i
+    sa.copy_(good)
+    sa[n // 3] = good[n // 3 + 1].item()   # one position twice, another missing
+    torch.cuda.synchronize()
+    assert dev.certify_sa()["violations"] >= 1
+    sa.copy_(good)
+    torch.cuda.synchronize()
+    assert dev.certify_sa()["violations"] == 0
+    del dev
+    gc.collect()
+    del bufs, sa, good

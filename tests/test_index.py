@@ -95,3 +95,53 @@ def test_threaded_bwt_from_sa_equals_host_build():
         assert list(c) == oi.occ4(k) == o2.occ4(k), k
     for r in [1, 32, 64, n - n % 32] + [32 * rng.randrange(1, n // 32) for _ in range(500)]:
         assert lib().bsq_index_sa(h, r) == oi.sa(r) == o2.sa(r), r
+
+
+def _sa_copy(rows, low_complexity=False):
+    pi = BwaIndex()
+    for k, t in enumerate(rows):
+        pi.add_ref_sequence(k + 1, NucleotideSequence.from_text(t))
+    pi.build(threads=3)
+    eb = ctypes.c_int()
+    p = lib().bsq_index_sa_data(pi.handle, ctypes.byref(eb))
+    n = lib().bsq_index_seq_len(pi.handle) + 1
+    import numpy as np
+    dt = np.uint32 if eb.value == 4 else np.uint64
+    return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8 * (n * eb.value))).contents).view(dt).copy(), eb.value
+
+
+def _certify(rows, sa, eb):
+    o = O.OracleIndex()
+    for k, t in enumerate(rows):
+        o.add_ref(k + 1, NucleotideSequence.from_text(t).raw)
+    rc = O.lib().orc_index_build_from_sa(o.h, sa.ctypes.data, eb)
+    return rc, int(O.lib().orc_sa_violations())
+
+
+@pytest.mark.parametrize("kind", ["random_big", "low_complexity"])
+def test_host_sa_certificate_rejects_corruption(kind):
+    """orc_index_build_from_sa certifies an outside SA (the C3/C4 parity fixtures take their
+    oracle tables from the GPU's SA): range + one primary row + strictly increasing adjacent suffixes, which
+    implies a permutation.  A correct SA passes with 0 violations; swapped rows, a duplicated row (which also
+    drops a position) and an out-of-range value are each rejected."""
+    rng = random.Random(17)
+    if kind == "random_big":   # >= 2^20 rows: the 16-thread certificate with job boundaries
+        rows = ["".join(rng.choice("ACGT") for _ in range(290_001)), "".join(rng.choice("ACGT") for _ in range(270_003))]
+    else:                      # long common prefixes: the word-at-a-time compare runs past many equal words
+        rows = ["A" * 3000, "ACGT" * 900, "GATTACA" * 300, "A" * 2999 + "C"]
+    sa, eb = _sa_copy(rows)
+    n = len(sa)
+    assert _certify(rows, sa, eb) == (0, 0)
+    for i in ([1, n // 2, n - 2] + [rng.randrange(1, n - 1) for _ in range(3)]):
+        bad = sa.copy()
+        bad[i], bad[i + 1] = bad[i + 1], bad[i]
+        rc, v = _certify(rows, bad, eb)
+        assert rc == -2 and v >= 1, (i, rc, v)
+    j = rng.randrange(2, n - 2)
+    dup = sa.copy()
+    dup[j] = dup[j + 1] if dup[j + 1] != 0 else dup[j - 1]   # position lost, another twice (primary kept)
+    rc, v = _certify(rows, dup, eb)
+    assert rc == -2 and v >= 1
+    oob = sa.copy()
+    oob[n // 3] = n + 5
+    assert _certify(rows, oob, eb)[0] == -1
