@@ -764,16 +764,15 @@ def main() -> int:
     if dist is not None and args.dist_backend == "nccl" and not cfg["seeding"]:
         import torch
         IDB = 128   # BSQ_XCHG_ID_BYTES
-        ids = torch.zeros(S * IDB, dtype=torch.uint8, device=xdev)
+        ids = torch.zeros(IDB, dtype=torch.uint8, device=xdev)
         if rank == 0:
-            raw = ctypes.create_string_buffer(S * IDB)
-            for k in range(S):
-                N.check(L.bsq_xchg_unique_id(ctypes.addressof(raw) + k * IDB))
+            raw = ctypes.create_string_buffer(IDB)
+            N.check(L.bsq_xchg_unique_id(raw))
             ids.copy_(torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8))
         dist.broadcast(ids, src=0)
-        idb = ctypes.create_string_buffer(bytes(ids.cpu().numpy()), S * IDB)
+        idb = ctypes.create_string_buffer(bytes(ids.cpu().numpy()), IDB)
         nx = ctypes.c_void_p()
-        hb.phase = "joining the exchange lanes"
+        hb.phase = "joining the exchange communicator"
         N.check(L.bsq_xchg_create(world, rank, gpu, idb, S, ctypes.byref(nx)))
     elif dist is not None:
         from bioseqdb_amd import dist as D
@@ -888,9 +887,10 @@ def main() -> int:
                               "last step)" if rounds else "barrier after every step"),
         },
         "exchange": ({
-            "path": ("bsq_xchg: per round and lane (= batch) an RCCL all-gather of the record counts, then every rank's "
-                     "read offsets, hits and CIGAR words ncclSend/ncclRecv to rank 0 over xGMI and its pinned D2H there; "
-                     "the batch's next round waits only for its own send"),
+            "path": ("bsq_xchg: one RCCL communicator and one exchange thread per rank issuing, in one fixed (round, lane) "
+                     "order on every rank, an all-gather of the record counts + status, then every rank's read offsets, "
+                     "hits and CIGAR words ncclSend/ncclRecv to rank 0 over xGMI and its pinned D2H there; a lane's next "
+                     "round waits only for its own send"),
             "lanes": S, "bytes_per_step": int((moved1.value - moved0.value) / max(args.steps, 1)),
             "bytes_side": "received by rank 0" if rank == 0 else "sent by this rank",
             "host_wait_ms_per_step_per_lane": round(xwait.value / max(args.steps, 1) / S, 3),

@@ -5,23 +5,21 @@
 // puts every row into its tuplestore), here rank 0.  Under torchrun each rank is a process, so the records cross
 // between processes by RCCL over xGMI.
 //
-// A rank aligns its shard as S concurrent batches, each a stream of rounds (bsq_batch_run_rounds' schedule: a batch
-// starts its next round as soon as its previous one ends).  Batch i of every rank is bound to lane i: one RCCL
-// communicator, one exchange stream.  After each round of batch i, lane i (1) all-gathers every rank's record
-// counts (4 x int64 per rank) and reads them on the host, then (2) each rank r > 0 sends its read offsets, hit
-// records and CIGAR words to rank 0 (ncclSend x3 in one group) while rank 0 receives all of them into HBM
-// (ncclRecv x3 per rank in one group) and copies them to pinned host memory on the lane's stream.  A lane's
-// operations are issued by its batch's host thread only, in the same order on every rank, so lanes never wait on
-// each other; the batch's next round waits (on the device) only for its own send to drain.  Rank 0's own records
-// reach its host memory inside bsq_batch_run as on one GPU.
-//
-// Built on the public C-ABI of bsq_api.cpp, bsq_internal.h's batch_records and RCCL.
+// The orchestration -- one exchange thread per rank issuing every (round, lane)'s header all-gather and send/recv in
+// one fixed global order, failure propagation through the header's status word -- is exchange_core.h's Core, shared
+// with the host-memory simulation of tests/xchg_sim.cpp.  This file is its RCCL transport: ONE communicator and ONE
+// HIP stream per rank (every collective of the rank in one order on one queue), per-lane receive buffers (rank 0's
+// view of each lane's last round), per-lane `packed`/`sent` events that order a send after its batch's pack and the
+// batch's next round after the send.  Host waits on the exchange stream poll with a deadline (BSQ_XCHG_TIMEOUT_S,
+// default 600 s); on a timeout, a transport error or a failure any rank reports, the communicator is aborted
+// (ncclCommAbort), so a broken rank ends the job instead of hanging it.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -30,10 +28,14 @@
 
 #include "../../include/bsq.h"
 #include "bsq_internal.h"
+#include "exchange_core.h"
 
 extern "C" void bsq_internal_set_error(const char *msg);
 
 namespace {
+
+using bsq::xchg::Parts;
+using bsq::xchg::Records;
 
 int fail(int rc, const std::string &m)
 {
@@ -51,137 +53,173 @@ int fail(int rc, const std::string &m)
         const ncclResult_t r_ = (x);                                                                         \
         if (r_ != ncclSuccess) return fail(BSQ_E_HIP, std::string(#x) + ": " + ncclGetErrorString(r_));      \
     } while (0)
-
-constexpr int64_t kAlign = 256;
-int64_t al(int64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
-
-// One rank's records of one round: read offsets (n_reads + 1), hits, CIGAR words; each part 256-B aligned.
-struct Parts {
-    int64_t n_reads = 0, n_hits = 0, n_cigar = 0;
-    int64_t off_bytes() const { return (n_reads + 1) * 8; }
-    int64_t hit_bytes() const { return n_hits * (int64_t)sizeof(bsq_hit); }
-    int64_t cig_bytes() const { return n_cigar * 4; }
-    int64_t o_hit() const { return al(off_bytes()); }
-    int64_t o_cig() const { return o_hit() + al(hit_bytes()); }
-    int64_t total() const { return o_cig() + al(cig_bytes()); }
-};
+// inside the transport: the message goes to the Core's error string
+#define THIP(x)                                                                                              \
+    do {                                                                                                     \
+        const hipError_t e_ = (x);                                                                           \
+        if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return BSQ_E_HIP; }    \
+    } while (0)
+#define TNCCL(x)                                                                                             \
+    do {                                                                                                     \
+        const ncclResult_t r_ = (x);                                                                         \
+        if (r_ != ncclSuccess) { err = std::string(#x) + ": " + ncclGetErrorString(r_); return BSQ_E_HIP; }  \
+    } while (0)
 
 struct Lane {
-    ncclComm_t comm = nullptr;
-    hipStream_t xs = nullptr;
-    hipEvent_t packed = nullptr;     // on the batch stream: this round's records are final
+    hipStream_t bs = nullptr;        // the lane's batch stream (set by every round's produce)
+    hipEvent_t packed = nullptr;     // on bs: the round's records are final
     hipEvent_t sent = nullptr;       // on xs: the send buffers may be overwritten
-    int64_t *hdr_dev = nullptr;      // world x {n_reads, n_hits, n_cigar, 0}
-    int64_t *hdr_host = nullptr;     // pinned
+    bool has_sent = false;
     uint8_t *send_dev = nullptr;     // staging of a host-resident view (a round with retried reads)
     int64_t send_cap = 0;
     uint8_t *recv_dev = nullptr;     // rank 0: every other rank's parts
     int64_t recv_cap = 0;
     uint8_t *recv_host = nullptr;    // rank 0: the same, pinned (the caller's view of the last round)
     int64_t recv_host_cap = 0;
-    std::vector<Parts> parts;        // per rank, last round
-    std::vector<int64_t> at;         // per rank: offset of its parts in recv_dev / recv_host
-    int64_t bytes = 0, rounds = 0;   // bytes received (rank 0) or sent (other ranks) over all rounds
+};
+
+template <typename T>
+int grow(T *&p, int64_t &cap, int64_t need, bool pinned, std::string &err)
+{
+    if (need <= cap) return BSQ_OK;
+    const int64_t c = std::max<int64_t>(need + need / 4, 1 << 20);
+    if (pinned) { hipHostFree(p); p = nullptr; THIP(hipHostMalloc((void **)&p, (size_t)c)); }
+    else { hipFree(p); p = nullptr; THIP(hipMalloc((void **)&p, (size_t)c)); }
+    cap = c;
+    return BSQ_OK;
+}
+
+class RcclTransport final : public bsq::xchg::Transport {
+  public:
+    int world_ = 1, rank_ = 0, device_ = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t xs = nullptr;
+    int64_t *hdr_dev = nullptr;    // world x 4
+    int64_t *hdr_host = nullptr;   // pinned
+    std::vector<Lane> lanes;
+    double timeout_s = 600;
+    bool aborted = false;
+
+    int world() const override { return world_; }
+    int rank() const override { return rank_; }
+
+    // host wait for everything issued on xs so far, with a deadline (a peer that never joins must not hang us)
+    int sync_xs(std::string &err)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; ++spin) {
+            const hipError_t e = hipStreamQuery(xs);
+            if (e == hipSuccess) return BSQ_OK;
+            if (e != hipErrorNotReady) { err = std::string("exchange stream: ") + hipGetErrorString(e); return BSQ_E_HIP; }
+            ncclResult_t async = ncclSuccess;
+            if (ncclCommGetAsyncError(comm, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress) {
+                err = std::string("RCCL: ") + ncclGetErrorString(async);
+                return BSQ_E_HIP;
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+                err = "timed out after " + std::to_string((int)timeout_s) + " s waiting for the other ranks (BSQ_XCHG_TIMEOUT_S)";
+                return BSQ_E_HIP;
+            }
+            if (spin < 2000) std::this_thread::yield();
+            else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+
+    int all_gather(int, const int64_t mine[4], int64_t *all, std::string &err) override
+    {
+        THIP(hipSetDevice(device_));
+        int64_t *h = hdr_host + 4 * rank_;
+        memcpy(h, mine, 32);
+        THIP(hipMemcpyAsync(hdr_dev + 4 * rank_, h, 32, hipMemcpyHostToDevice, xs));
+        TNCCL(ncclAllGather(hdr_dev + 4 * rank_, hdr_dev, 4, ncclInt64, comm, xs));
+        THIP(hipMemcpyAsync(hdr_host, hdr_dev, (size_t)world_ * 32, hipMemcpyDeviceToHost, xs));
+        if (const int rc = sync_xs(err)) return rc;
+        memcpy(all, hdr_host, (size_t)world_ * 32);
+        return BSQ_OK;
+    }
+
+    int send(int li, const Records &r, const Parts &p, std::string &err) override
+    {
+        Lane &l = lanes[(size_t)li];
+        THIP(hipSetDevice(device_));
+        const void *off = r.off, *hits = r.hits, *cig = r.cig;
+        if (!r.on_device) {   // the view is in pinned host memory: stage it in HBM first (same stream)
+            if (p.total() > l.send_cap) { if (const int rc = sync_xs(err)) return rc; }   // the old buffer may be in flight
+            if (const int rc = grow(l.send_dev, l.send_cap, p.total(), false, err)) return rc;
+            THIP(hipMemcpyAsync(l.send_dev, r.off, (size_t)p.off_bytes(), hipMemcpyHostToDevice, xs));
+            if (p.n_hits) THIP(hipMemcpyAsync(l.send_dev + p.o_hit(), r.hits, (size_t)p.hits_bytes(), hipMemcpyHostToDevice, xs));
+            if (p.n_cigar) THIP(hipMemcpyAsync(l.send_dev + p.o_cig(), r.cig, (size_t)p.cig_bytes(), hipMemcpyHostToDevice, xs));
+            off = l.send_dev; hits = l.send_dev + p.o_hit(); cig = l.send_dev + p.o_cig();
+            // the batch's next run may regrow (free) the pinned view these copies read
+            if (const int rc = sync_xs(err)) return rc;
+        } else {   // straight from the batch's packed arrays: the send waits for the batch stream's pack
+            THIP(hipStreamWaitEvent(xs, l.packed, 0));
+        }
+        TNCCL(ncclGroupStart());
+        TNCCL(ncclSend(off, (size_t)p.off_bytes(), ncclUint8, 0, comm, xs));
+        if (p.n_hits) TNCCL(ncclSend(hits, (size_t)p.hits_bytes(), ncclUint8, 0, comm, xs));
+        if (p.n_cigar) TNCCL(ncclSend(cig, (size_t)p.cig_bytes(), ncclUint8, 0, comm, xs));
+        TNCCL(ncclGroupEnd());
+        THIP(hipEventRecord(l.sent, xs));
+        l.has_sent = true;
+        return BSQ_OK;
+    }
+
+    int recv(int li, const std::vector<Parts> &parts, const std::vector<int64_t> &at, int64_t total, std::string &err) override
+    {
+        Lane &l = lanes[(size_t)li];
+        THIP(hipSetDevice(device_));
+        if (total > l.recv_cap || total > l.recv_host_cap) { if (const int rc = sync_xs(err)) return rc; }
+        if (const int rc = grow(l.recv_dev, l.recv_cap, total, false, err)) return rc;
+        if (const int rc = grow(l.recv_host, l.recv_host_cap, total, true, err)) return rc;
+        TNCCL(ncclGroupStart());
+        for (int k = 1; k < world_; ++k) {
+            const Parts &p = parts[(size_t)k];
+            uint8_t *d = l.recv_dev + at[(size_t)k];
+            TNCCL(ncclRecv(d, (size_t)p.off_bytes(), ncclUint8, k, comm, xs));
+            if (p.n_hits) TNCCL(ncclRecv(d + p.o_hit(), (size_t)p.hits_bytes(), ncclUint8, k, comm, xs));
+            if (p.n_cigar) TNCCL(ncclRecv(d + p.o_cig(), (size_t)p.cig_bytes(), ncclUint8, k, comm, xs));
+        }
+        TNCCL(ncclGroupEnd());
+        if (total) THIP(hipMemcpyAsync(l.recv_host, l.recv_dev, (size_t)total, hipMemcpyDeviceToHost, xs));
+        return BSQ_OK;
+    }
+
+    int batch_resume(int li, std::string &err) override
+    {
+        Lane &l = lanes[(size_t)li];
+        if (l.has_sent && l.bs) THIP(hipStreamWaitEvent(l.bs, l.sent, 0));   // the next round overwrites the sent arrays
+        return BSQ_OK;
+    }
+
+    void abort() override
+    {
+        if (comm && !aborted) ncclCommAbort(comm);
+        aborted = true;
+        comm = nullptr;
+    }
+
+    ~RcclTransport()
+    {
+        hipSetDevice(device_);
+        if (xs && !aborted) hipStreamSynchronize(xs);
+        if (comm) ncclCommDestroy(comm);
+        for (Lane &l : lanes) {
+            hipFree(l.send_dev); hipFree(l.recv_dev); hipHostFree(l.recv_host);
+            if (l.packed) hipEventDestroy(l.packed);
+            if (l.sent) hipEventDestroy(l.sent);
+        }
+        hipFree(hdr_dev); hipHostFree(hdr_host);
+        if (xs) hipStreamDestroy(xs);
+    }
 };
 
 }  // namespace
 
 struct bsq_xchg {
-    int world = 1, rank = 0, device = 0;
-    std::vector<Lane> lanes;
-    double wait_ms = 0;               // host time the batch threads spent in the exchange (all lanes)
+    std::unique_ptr<RcclTransport> t;
+    std::unique_ptr<bsq::xchg::Core> core;
 };
-
-namespace {
-
-void free_lane(Lane &l)
-{
-    if (l.xs) hipStreamSynchronize(l.xs);
-    if (l.comm) ncclCommDestroy(l.comm);
-    hipFree(l.hdr_dev); hipHostFree(l.hdr_host); hipFree(l.send_dev); hipFree(l.recv_dev); hipHostFree(l.recv_host);
-    if (l.packed) hipEventDestroy(l.packed);
-    if (l.sent) hipEventDestroy(l.sent);
-    if (l.xs) hipStreamDestroy(l.xs);
-    l = Lane{};
-}
-
-template <typename T>
-int grow(T *&p, int64_t &cap, int64_t need, bool pinned)
-{
-    if (need <= cap) return BSQ_OK;
-    const int64_t c = std::max<int64_t>(need + need / 4, 1 << 20);
-    if (pinned) { hipHostFree(p); p = nullptr; XHIP(hipHostMalloc((void **)&p, (size_t)c)); }
-    else { hipFree(p); p = nullptr; XHIP(hipMalloc((void **)&p, (size_t)c)); }
-    cap = c;
-    return BSQ_OK;
-}
-
-// The exchange of one round of lane `li`'s batch (called by that batch's host thread right after bsq_batch_run).
-int lane_round(bsq_xchg *x, int li, bsq_batch *b)
-{
-    Lane &l = x->lanes[(size_t)li];
-    const bsq::BatchRecords r = bsq::batch_records(b);
-    hipStream_t bs = static_cast<hipStream_t>(r.stream);
-    XHIP(hipSetDevice(x->device));
-    // (1) every rank's counts, on the host of every rank
-    int64_t *mine = l.hdr_host + 4 * x->rank;
-    mine[0] = r.n_reads; mine[1] = r.n_hits; mine[2] = r.n_cigar; mine[3] = 0;
-    XHIP(hipMemcpyAsync(l.hdr_dev + 4 * x->rank, mine, 32, hipMemcpyHostToDevice, l.xs));
-    XNCCL(ncclAllGather(l.hdr_dev + 4 * x->rank, l.hdr_dev, 4, ncclInt64, l.comm, l.xs));
-    XHIP(hipMemcpyAsync(l.hdr_host, l.hdr_dev, (size_t)x->world * 32, hipMemcpyDeviceToHost, l.xs));
-    XHIP(hipStreamSynchronize(l.xs));
-    int64_t total = 0;
-    for (int k = 0; k < x->world; ++k) {
-        Parts &p = l.parts[(size_t)k];
-        p.n_reads = l.hdr_host[4 * k]; p.n_hits = l.hdr_host[4 * k + 1]; p.n_cigar = l.hdr_host[4 * k + 2];
-        l.at[(size_t)k] = total;
-        if (k != 0) total += p.total();
-    }
-    ++l.rounds;
-    if (x->world == 1) return BSQ_OK;
-    const ncclDataType_t u8 = ncclUint8;
-    if (x->rank != 0) {   // (2) send this rank's parts to rank 0
-        const Parts &p = l.parts[(size_t)x->rank];
-        const void *off = r.off, *hits = r.hits, *cig = r.cig;
-        if (!r.on_device) {   // the view is in pinned host memory: stage it in HBM first (same stream)
-            { const int rc = grow(l.send_dev, l.send_cap, p.total(), false); if (rc) return rc; }
-            XHIP(hipMemcpyAsync(l.send_dev, r.off, (size_t)p.off_bytes(), hipMemcpyHostToDevice, l.xs));
-            if (p.n_hits) XHIP(hipMemcpyAsync(l.send_dev + p.o_hit(), r.hits, (size_t)p.hit_bytes(), hipMemcpyHostToDevice, l.xs));
-            if (p.n_cigar) XHIP(hipMemcpyAsync(l.send_dev + p.o_cig(), r.cig, (size_t)p.cig_bytes(), hipMemcpyHostToDevice, l.xs));
-            off = l.send_dev; hits = l.send_dev + p.o_hit(); cig = l.send_dev + p.o_cig();
-            XHIP(hipStreamSynchronize(l.xs));   // the next run may regrow (free) the pinned view it copies from
-        } else {   // straight from the batch's packed arrays: the lane waits for the batch stream's pack
-            XHIP(hipEventRecord(l.packed, bs));
-            XHIP(hipStreamWaitEvent(l.xs, l.packed, 0));
-        }
-        XNCCL(ncclGroupStart());
-        XNCCL(ncclSend(off, (size_t)p.off_bytes(), u8, 0, l.comm, l.xs));
-        if (p.n_hits) XNCCL(ncclSend(hits, (size_t)p.hit_bytes(), u8, 0, l.comm, l.xs));
-        if (p.n_cigar) XNCCL(ncclSend(cig, (size_t)p.cig_bytes(), u8, 0, l.comm, l.xs));
-        XNCCL(ncclGroupEnd());
-        XHIP(hipEventRecord(l.sent, l.xs));
-        XHIP(hipStreamWaitEvent(bs, l.sent, 0));   // the batch's next round overwrites the sent arrays
-        l.bytes += p.off_bytes() + p.hit_bytes() + p.cig_bytes();
-        return BSQ_OK;
-    }
-    // rank 0: receive every other rank's parts into HBM, then into pinned host memory
-    { const int rc = grow(l.recv_dev, l.recv_cap, total, false); if (rc) return rc; }
-    { const int rc = grow(l.recv_host, l.recv_host_cap, total, true); if (rc) return rc; }
-    XNCCL(ncclGroupStart());
-    for (int k = 1; k < x->world; ++k) {
-        const Parts &p = l.parts[(size_t)k];
-        uint8_t *d = l.recv_dev + l.at[(size_t)k];
-        XNCCL(ncclRecv(d, (size_t)p.off_bytes(), u8, k, l.comm, l.xs));
-        if (p.n_hits) XNCCL(ncclRecv(d + p.o_hit(), (size_t)p.hit_bytes(), u8, k, l.comm, l.xs));
-        if (p.n_cigar) XNCCL(ncclRecv(d + p.o_cig(), (size_t)p.cig_bytes(), u8, k, l.comm, l.xs));
-    }
-    XNCCL(ncclGroupEnd());
-    if (total) XHIP(hipMemcpyAsync(l.recv_host, l.recv_dev, (size_t)total, hipMemcpyDeviceToHost, l.xs));
-    l.bytes += total;
-    return BSQ_OK;
-}
-
-}  // namespace
 
 extern "C" int bsq_xchg_unique_id(void *id)
 {
@@ -192,9 +230,9 @@ extern "C" int bsq_xchg_unique_id(void *id)
     return BSQ_OK;
 }
 
-extern "C" int bsq_xchg_create(int world, int rank, int device, const void *ids, int lanes, bsq_xchg **out)
+extern "C" int bsq_xchg_create(int world, int rank, int device, const void *id, int lanes, bsq_xchg **out)
 {
-    if (!out || !ids || world < 1 || rank < 0 || rank >= world || lanes < 1 || lanes > 64)
+    if (!out || !id || world < 1 || rank < 0 || rank >= world || lanes < 1 || lanes > 64)
         return fail(BSQ_E_INVALID, "invalid argument");
     *out = nullptr;
     int ndev = 0;
@@ -202,30 +240,23 @@ extern "C" int bsq_xchg_create(int world, int rank, int device, const void *ids,
         return fail(BSQ_E_NODEV, "no HIP device " + std::to_string(device));
     std::unique_ptr<bsq_xchg> x(new (std::nothrow) bsq_xchg());
     if (!x) return fail(BSQ_E_NOMEM, "out of memory");
-    x->world = world; x->rank = rank; x->device = device;
-    x->lanes.resize((size_t)lanes);
+    x->t.reset(new RcclTransport());
+    RcclTransport &t = *x->t;
+    t.world_ = world; t.rank_ = rank; t.device_ = device;
+    if (const char *s = getenv("BSQ_XCHG_TIMEOUT_S")) { const double v = atof(s); if (v > 0) t.timeout_s = v; }
     XHIP(hipSetDevice(device));
-    auto cleanup = [&] { for (Lane &l : x->lanes) free_lane(l); };
-    for (Lane &l : x->lanes) {
-        l.parts.resize((size_t)world);
-        l.at.resize((size_t)world);
-        hipError_t e = hipStreamCreateWithFlags(&l.xs, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&l.packed, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&l.sent, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipMalloc(&l.hdr_dev, (size_t)world * 32);
-        if (e == hipSuccess) e = hipHostMalloc((void **)&l.hdr_host, (size_t)world * 32);
-        if (e != hipSuccess) { cleanup(); return fail(BSQ_E_HIP, std::string("exchange lane: ") + hipGetErrorString(e)); }
+    XHIP(hipStreamCreateWithFlags(&t.xs, hipStreamNonBlocking));
+    XHIP(hipMalloc(&t.hdr_dev, (size_t)world * 32));
+    XHIP(hipHostMalloc((void **)&t.hdr_host, (size_t)world * 32));
+    t.lanes.resize((size_t)lanes);
+    for (Lane &l : t.lanes) {
+        XHIP(hipEventCreateWithFlags(&l.packed, hipEventDisableTiming));
+        XHIP(hipEventCreateWithFlags(&l.sent, hipEventDisableTiming));
     }
-    // every lane's communicator in one group (the ranks join lane by lane in the same order)
-    ncclResult_t r = ncclGroupStart();
-    for (int k = 0; k < lanes && r == ncclSuccess; ++k) {
-        ncclUniqueId u;
-        memcpy(&u, static_cast<const uint8_t *>(ids) + (size_t)k * sizeof u, sizeof u);
-        r = ncclCommInitRank(&x->lanes[(size_t)k].comm, world, u, rank);
-    }
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r == ncclSuccess) r = r2;
-    if (r != ncclSuccess) { cleanup(); return fail(BSQ_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    XNCCL(ncclCommInitRank(&t.comm, world, u, rank));
+    x->core.reset(new bsq::xchg::Core(t, lanes, (int64_t)sizeof(bsq_hit)));
     *out = x.release();
     return BSQ_OK;
 }
@@ -233,8 +264,8 @@ extern "C" int bsq_xchg_create(int world, int rank, int device, const void *ids,
 extern "C" void bsq_xchg_free(bsq_xchg *x)
 {
     if (!x) return;
-    hipSetDevice(x->device);
-    for (Lane &l : x->lanes) free_lane(l);
+    x->core.reset();
+    x->t.reset();
     delete x;
 }
 
@@ -243,55 +274,60 @@ extern "C" int bsq_batch_run_rounds_x(bsq_batch *const *batches, int n, const bs
 {
     if (!x) return bsq_batch_run_rounds(batches, n, opts, first_call, rounds);
     if (n < 1 || rounds < 0 || !batches || !opts || !first_call) return fail(BSQ_E_INVALID, "invalid argument");
-    if (n != (int)x->lanes.size()) return fail(BSQ_E_INVALID, "one exchange lane per batch expected");
-    std::vector<int> rc((size_t)n, BSQ_OK);
+    if (n != x->core->n_lanes()) return fail(BSQ_E_INVALID, "one exchange lane per batch expected");
+    if (x->core->aborted()) return fail(BSQ_E_INVALID, "the exchange was aborted by an earlier failure");
+    RcclTransport &t = *x->t;
     std::vector<std::string> msg((size_t)n);
-    std::vector<double> wait((size_t)n, 0.0);
-    auto one = [&](int i) {
-        roctxRangePushA("bsq_batch_rounds_x");
-        for (int k = 0; k < rounds && !rc[(size_t)i]; ++k) {
-            rc[(size_t)i] = bsq_batch_run(batches[i], opts, first_call[i]);
-            if (rc[(size_t)i]) break;
-            const auto t0 = std::chrono::steady_clock::now();
-            rc[(size_t)i] = lane_round(x, i, batches[i]);
-            wait[(size_t)i] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    auto produce = [&](int i, int, Records &rec) -> int {
+        roctxRangePushA("bsq_batch_round_x");
+        int rc = bsq_batch_run(batches[i], opts, first_call[i]);
+        if (!rc) {
+            const bsq::BatchRecords r = bsq::batch_records(batches[i]);
+            Lane &l = t.lanes[(size_t)i];
+            l.bs = static_cast<hipStream_t>(r.stream);
+            if (hipEventRecord(l.packed, l.bs) != hipSuccess) { rc = BSQ_E_HIP; bsq_internal_set_error("hipEventRecord(packed)"); }
+            rec.n_reads = r.n_reads; rec.n_hits = r.n_hits; rec.n_cigar = r.n_cigar;
+            rec.off = r.off; rec.hits = r.hits; rec.cig = r.cig; rec.on_device = r.on_device;
         }
-        if (rc[(size_t)i]) msg[(size_t)i] = bsq_last_error();
+        if (rc) msg[(size_t)i] = bsq_last_error();
         roctxRangePop();
+        return rc;
     };
-    std::vector<std::thread> th;
-    for (int i = 1; i < n; ++i) th.emplace_back(one, i);
-    one(0);
-    for (auto &t : th) t.join();
-    for (double w : wait) x->wait_ms += w;
-    for (int i = 0; i < n; ++i)
-        if (rc[(size_t)i]) return fail(rc[(size_t)i], "batch " + std::to_string(i) + ": " + msg[(size_t)i]);
+    std::string err;
+    const int rc = x->core->run(rounds, produce, err);
+    if (rc) {
+        for (int i = 0; i < n; ++i)
+            if (!msg[(size_t)i].empty()) err += "; local batch " + std::to_string(i) + ": " + msg[(size_t)i];
+        return fail(rc, err);
+    }
     return BSQ_OK;
 }
 
 extern "C" int bsq_xchg_finish(bsq_xchg *x, int64_t *bytes_moved, double *wait_ms)
 {
     if (!x) return fail(BSQ_E_INVALID, "invalid argument");
-    XHIP(hipSetDevice(x->device));
-    int64_t moved = 0;
-    for (Lane &l : x->lanes) {
-        XHIP(hipStreamSynchronize(l.xs));
-        moved += l.bytes;
+    RcclTransport &t = *x->t;
+    XHIP(hipSetDevice(t.device_));
+    if (!x->core->aborted()) {
+        std::string err;
+        if (const int rc = t.sync_xs(err)) { t.abort(); return fail(rc, err); }
     }
+    int64_t moved = 0;
+    for (int i = 0; i < x->core->n_lanes(); ++i) moved += x->core->lane(i).bytes;
     if (bytes_moved) *bytes_moved = moved;
-    if (wait_ms) *wait_ms = x->wait_ms;
+    if (wait_ms) *wait_ms = x->core->wait_ms();
     return BSQ_OK;
 }
 
 extern "C" int bsq_xchg_view(const bsq_xchg *x, int lane, int src_rank, bsq_hits *out)
 {
-    if (!x || !out || lane < 0 || lane >= (int)x->lanes.size() || src_rank < 0 || src_rank >= x->world)
+    if (!x || !out || lane < 0 || lane >= x->core->n_lanes() || src_rank < 0 || src_rank >= x->t->world_)
         return fail(BSQ_E_INVALID, "invalid argument");
-    if (x->rank != 0 || src_rank == 0) return fail(BSQ_E_INVALID, "rank 0 holds the other ranks' records (its own are in its batches)");
-    const Lane &l = x->lanes[(size_t)lane];
-    if (!l.rounds) return fail(BSQ_E_INVALID, "no round exchanged yet");
-    const Parts &p = l.parts[(size_t)src_rank];
-    uint8_t *h = l.recv_host + l.at[(size_t)src_rank];
+    if (x->t->rank_ != 0 || src_rank == 0) return fail(BSQ_E_INVALID, "rank 0 holds the other ranks' records (its own are in its batches)");
+    const bsq::xchg::LaneState &ls = x->core->lane(lane);
+    if (!ls.rounds) return fail(BSQ_E_INVALID, "no round exchanged yet");
+    const Parts &p = ls.parts[(size_t)src_rank];
+    uint8_t *h = x->t->lanes[(size_t)lane].recv_host + ls.at[(size_t)src_rank];
     *out = bsq_hits{};
     out->n_reads = (int32_t)p.n_reads;
     out->n_hits = p.n_hits;

@@ -218,19 +218,22 @@ int bsq_group_render_nuclseqs(bsq_group *g, const void *const *reads, uint8_t **
 
 /* ---- One process per GPU (torchrun): the record exchange to rank 0 ----
  * Every rank's hit records return to the caller (rank 0), the rows nuclseq_multi_search_bwa puts into its
- * tuplestore (extension.cpp:362-370).  Lane i (one RCCL communicator + stream) carries batch i of every rank:
- * after each round the lane all-gathers the ranks' record counts, every rank r > 0 sends its read offsets, hits
- * and CIGAR words to rank 0 (ncclSend/ncclRecv over xGMI) and rank 0 copies them to pinned host memory. */
+ * tuplestore (extension.cpp:362-370).  Batch i of a rank is lane i.  After each round of each lane, ONE exchange
+ * thread per rank -- in the same (round, lane) order on every rank, on one RCCL communicator and one stream, so
+ * operations match one-to-one and cannot deadlock -- all-gathers the ranks' record counts and batch status, then
+ * every rank r > 0 sends its read offsets, hits and CIGAR words to rank 0 (ncclSend/ncclRecv over xGMI) and rank 0
+ * copies them to pinned host memory.  A batch failure on any rank stops every rank at that same (round, lane);
+ * a peer silent for BSQ_XCHG_TIMEOUT_S seconds (default 600) aborts the communicator instead of hanging. */
 typedef struct bsq_xchg bsq_xchg;
 #define BSQ_XCHG_ID_BYTES 128
-/* A fresh communicator id (BSQ_XCHG_ID_BYTES bytes) -- rank 0 makes one per lane and the launcher's own channel
- * (torch.distributed) hands them to every rank. */
+/* A fresh communicator id (BSQ_XCHG_ID_BYTES bytes) -- rank 0 makes it and the launcher's own channel
+ * (torch.distributed) hands it to every rank. */
 int bsq_xchg_unique_id(void *id);
-/* Joins the `lanes` communicators (ids: lanes x BSQ_XCHG_ID_BYTES, the same on every rank) on `device`; collective. */
-int bsq_xchg_create(int world, int rank, int device, const void *ids, int lanes, bsq_xchg **out);
+/* Joins the communicator `id` (BSQ_XCHG_ID_BYTES, the same on every rank) with `lanes` lanes on `device`; collective. */
+int bsq_xchg_create(int world, int rank, int device, const void *id, int lanes, bsq_xchg **out);
 void bsq_xchg_free(bsq_xchg *x);
 /* bsq_batch_run_rounds with lane i exchanging batch i's records after every round (n == lanes on every rank);
- * x == NULL: bsq_batch_run_rounds. */
+ * x == NULL: bsq_batch_run_rounds.  After a failure (any rank's) the exchange is aborted and later calls fail. */
 int bsq_batch_run_rounds_x(bsq_batch *const *batches, int n, const bsq_opts *opts, const uint64_t *first_call,
                            int rounds, bsq_xchg *x);
 /* Waits for every lane's last exchange (rank 0: the records are in its host memory).  *bytes_moved: bytes

@@ -96,6 +96,48 @@ def test_c2_100mbp_seeding(c3_pair):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("exchange", [0, 1])
+def test_c3_100mbp_replicated_group_8(c3_pair, exchange):
+    """C5's sharding at the C3 index on the one-GPU box: an 8-member device group (device 0
+    listed 8 times: replicas by device-to-device copies), 24,003 reads split into 8 ragged shares, the lrand48
+    stream continuing from an earlier call (member k starts at first_call + k*n/8), records over every member's
+    link (exchange 0) or gathered in member 0's HBM first (exchange 1), one barrier-free stream of 2 rounds.  Every
+    column equals the oracle's rows; the segments come back in member order at the shares' first reads."""
+    ref, pi, oi = c3_pair
+    from parity_util import _oracle_batch_tsv, compare_tsv
+    reads = synth.make_reads(ref, 24_003, seed=synth.READ_SEED + 11)
+    seqs = _seqs(reads)
+    n = len(seqs)
+    G = 8
+    ptrs = (ctypes.c_void_p * n)(*[s.ptr for s in seqs])
+    L = N.lib()
+    g = ctypes.c_void_p()
+    N.check(L.bsq_group_create((ctypes.c_int * G)(*([0] * G)), G, ctypes.byref(g)))
+    try:
+        N.check(L.bsq_group_set_exchange(g, exchange))
+        N.check(L.bsq_group_replicate(g, pi.handle, None))
+        first_call = 40_000
+        N.check(L.bsq_group_run(g, ctypes.byref(pi.options), ptrs, n, first_call))
+        N.check(L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n, first_call, 2))
+        segs = (ctypes.POINTER(N.Hits) * 64)()
+        slo = (ctypes.c_int32 * 64)()
+        ns = L.bsq_group_segments(g, segs, slo, 64)
+        lo = [k * n // G for k in range(G)]
+        assert ns >= G and sorted(set(slo[:ns])) == list(slo[:ns]) and set(lo) <= set(slo[:ns]), list(slo[:ns])
+        assert sum(segs[i].contents.n_reads for i in range(ns)) == n
+        H = L.bsq_group_hits(g)
+        p = L.bsq_render_tsv(pi.handle, H, ptrs)
+        text = ctypes.string_at(p).decode("latin-1")
+        L.bsq_free(p)
+        counts = [H.contents.read_off[i + 1] - H.contents.read_off[i] for i in range(n)]
+    finally:
+        L.bsq_group_free(g)
+    exp, ec = _oracle_batch_tsv(oi, O.opts_from(pi.options), [s.raw for s in seqs], first_call)
+    rows, bad = compare_tsv(text, counts, exp, ec)
+    assert rows > 22_000
+    assert not bad, bad[:20]
+
+
 # ---- the bwa_options surface (bwa_opts() arguments, Q1 applied by bwa_opts) -------------------------
 OPTION_SETS = {
     "q2_match2_mismatch3": dict(match_score=2, mismatch_penalty=3),
