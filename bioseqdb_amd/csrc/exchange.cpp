@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -278,9 +279,13 @@ extern "C" int bsq_batch_run_rounds_x(bsq_batch *const *batches, int n, const bs
     if (x->core->aborted()) return fail(BSQ_E_INVALID, "the exchange was aborted by an earlier failure");
     RcclTransport &t = *x->t;
     std::vector<std::string> msg((size_t)n);
-    auto produce = [&](int i, int, Records &rec) -> int {
+    // fault injection for the failure path's tests: BSQ_XCHG_TEST_FAIL="lane:round" fails that batch run on this rank
+    int fail_lane = -1, fail_round = -1;
+    if (const char *f = getenv("BSQ_XCHG_TEST_FAIL")) sscanf(f, "%d:%d", &fail_lane, &fail_round);
+    auto produce = [&](int i, int k, Records &rec) -> int {
         roctxRangePushA("bsq_batch_round_x");
-        int rc = bsq_batch_run(batches[i], opts, first_call[i]);
+        int rc = (i == fail_lane && k == fail_round) ? (bsq_internal_set_error("injected failure (BSQ_XCHG_TEST_FAIL)"), BSQ_E_INVALID)
+                                                     : bsq_batch_run(batches[i], opts, first_call[i]);
         if (!rc) {
             const bsq::BatchRecords r = bsq::batch_records(batches[i]);
             Lane &l = t.lanes[(size_t)i];

@@ -82,3 +82,16 @@ def test_native_exchange_world1_stream_of_rounds():
     assert "stream of batch runs" in x["config"]["step_schedule"]
     one = _bench("--timed-only")
     assert x["checksums"] == one["checksums"]
+
+
+def test_native_exchange_failure_stops_cleanly():
+    """A batch failure inside the exchanged stream of rounds (injected on lane 2, round 1 by BSQ_XCHG_TEST_FAIL) is
+    carried by the header all-gather's status word: the run stops at that (round, lane), the RCCL communicator is
+    aborted, and bench.py exits non-zero naming it -- instead of the other lanes (and, with more ranks, the other
+    ranks) waiting forever in their collectives."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", BSQ_XCHG_TEST_FAIL="2:1", BSQ_XCHG_TIMEOUT_S="60")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--exchange-world1", "--timed-only"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0
+    assert "rank 0 lane 2 round 1 failed" in r.stderr and "injected failure" in r.stderr, r.stderr[-3000:]
