@@ -1051,7 +1051,10 @@ def main() -> int:
 
         t_sub, sub_s = [0.0], [0.0]
 
-        def cursor(cols):
+        def cursor(cols, deferred=True):
+            # deferred (the drop-in's loop since round 5, extension_bsq.cpp for_each_fetch_held): fetch k is staged by a
+            # pipeline worker, and its tuples are "freed" after fetch k+1 is submitted and k's staging has finished;
+            # copy: staged on the caller's thread inside bsq_pipeline_submit (round 4)
             p = ctypes.c_void_p()
             N.check(L.bsq_pipeline_create(idx, depth, ctypes.byref(p)))
             try:
@@ -1059,7 +1062,7 @@ def main() -> int:
                 for rep in range(3):   # first pass allocates the slots' workspaces
                     t_sub[0] = 0.0
                     t1 = time.perf_counter()
-                    pend, rows = 0, 0
+                    pend, rows, held = 0, 0, -1
 
                     def take():
                         v = ctypes.POINTER(N.Hits)()
@@ -1074,9 +1077,19 @@ def main() -> int:
                         n = min(fetch, reads.n - r0)
                         sp = ctypes.cast(ctypes.addressof(ptrs) + r0 * ctypes.sizeof(ctypes.c_void_p), ctypes.c_void_p)
                         t2 = time.perf_counter()
-                        N.check(L.bsq_pipeline_submit(p, ctypes.byref(opts), sp, n, first_call + lo, cols))
+                        if deferred:
+                            tk = ctypes.c_int64()
+                            N.check(L.bsq_pipeline_submit_deferred(p, ctypes.byref(opts), sp, n, first_call + lo, cols,
+                                                                   ctypes.byref(tk)))
+                            if held >= 0:
+                                N.check(L.bsq_pipeline_wait_staged(p, held + 1))
+                            held = tk.value
+                        else:
+                            N.check(L.bsq_pipeline_submit(p, ctypes.byref(opts), sp, n, first_call + lo, cols))
                         t_sub[0] += time.perf_counter() - t2
                         pend += 1
+                    if held >= 0:
+                        N.check(L.bsq_pipeline_wait_staged(p, held + 1))
                     while pend:
                         rows += take()
                         pend -= 1
@@ -1092,16 +1105,19 @@ def main() -> int:
         sub_c = sub_s[0]
         rows_r, dt_r = cursor(0)
         sub_r = sub_s[0]
+        rows_cc, dt_cc = cursor(1, deferred=False)
         nr = passes * reads.n
         result["sql_cursor"] = {
             "reads": nr, "fetch_rows": fetch, "depth": depth,
             "reads_per_s_with_columns": round(nr / dt_c, 1), "reads_per_s_records_only": round(nr / dt_r, 1),
-            "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits,
+            "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits and rows_cc == passes * n_hits,
             "submit_s": [round(sub_c, 4), round(sub_r, 4)], "loop_s": [round(dt_c, 4), round(dt_r, 4)],
-            "note": "bsq_pipeline over fetches of host nuclseq varlenas (staging on the caller's thread, upload, "
-                    "alignment, D2H, and with columns the two nuclseq columns of every row on the GPU), as "
-                    "extension_bsq.cpp's cursor loop runs it, over a cursor of the batch's reads 4 times (lrand48 "
-                    "positions continuing); best of 2 runs after a warm-up run"}
+            "copy_staging_reads_per_s_with_columns": round(nr / dt_cc, 1),
+            "note": "bsq_pipeline over fetches of host nuclseq varlenas (deferred submissions: staged by the pipeline's "
+                    "workers while the caller submits the next fetch, then upload, alignment, D2H, and with columns the "
+                    "two nuclseq columns of every row on the GPU), as extension_bsq.cpp's cursor loop runs it, over a "
+                    "cursor of the batch's reads 4 times (lrand48 positions continuing); best of 2 runs after a warm-up "
+                    "run; copy_staging_*: the same with the staging on the caller's thread (round 4's loop)"}
         # beside the headline: the drop-in's own call path (the pipelined cursor loop, columns included)
         result["value_sql_call"] = round(nr / dt_c, 1)
         del keep, ptrs

@@ -157,6 +157,9 @@ SIGNATURES = {
     "bsq_pipeline_next": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(Hits)), ctypes.POINTER(_P),
                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))]),
     "bsq_pipeline_release": (ctypes.c_int, [_P]),
+    "bsq_pipeline_submit_deferred": (ctypes.c_int, [_P, ctypes.POINTER(Opts), _P, ctypes.c_int32, ctypes.c_uint64,
+                                                    ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+    "bsq_pipeline_wait_staged": (ctypes.c_int, [_P, ctypes.c_int64]),
 }
 
 _lib = None

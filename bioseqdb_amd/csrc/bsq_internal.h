@@ -65,6 +65,8 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
 // With nothing outstanding, the next submission goes to slot 0 again (a caller that submits shares j = 0..s-1 per
 // round keeps share j on slot j, where a RERUN finds its staging).  BSQ_E_INVALID while submissions are pending.
 int pipeline_rewind(bsq_pipeline *p);
+// every DEFER submission numbered < upto has stopped reading its caller's varlenas
+int pipeline_wait_staged(bsq_pipeline *p, int64_t upto);
 // Record route of every batch of the pipeline (bsq_batch_set_record_route; -1: each batch's own device link).
 // BSQ_E_INVALID while submissions are pending.
 int pipeline_set_record_route(bsq_pipeline *p, int via_device);

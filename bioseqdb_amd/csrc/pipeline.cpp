@@ -45,6 +45,7 @@ struct Slot {
     bool cols = false;
     PipeMode mode = PipeMode::COPY;
     const void *const *reads = nullptr;   // PipeMode::DEFER: staged by the worker
+    bool stage_pending = false;           // DEFER: the caller's reads are still referenced (bsq_pipeline_wait_staged)
     // batch and staging
     bsq_batch *batch = nullptr;
     int32_t cap_reads = 0;
@@ -104,11 +105,24 @@ int prep_job(bsq_pipeline *p, Slot &x)
 {
     x.t[1] = now_ms();
     if (const char *e = getenv("BSQ_PIPE_FAILPOINT")) {   // tests: job number e fails here (a failed fetch)
-        if (*e && strtoull(e, nullptr, 10) == x.job) { set_error("injected failure (BSQ_PIPE_FAILPOINT)"); return BSQ_E_INVALID; }
+        if (*e && strtoull(e, nullptr, 10) == x.job) {
+            std::lock_guard<std::mutex> lk(p->mu);
+            x.stage_pending = false;
+            x.reads = nullptr;
+            p->cv.notify_all();
+            set_error("injected failure (BSQ_PIPE_FAILPOINT)");
+            return BSQ_E_INVALID;
+        }
     }
     if (x.mode == PipeMode::DEFER) {
         x.resident = false;
         const int rc = stage_nuclseqs(x.stage, x.reads, x.n);
+        {   // the caller's varlenas are no longer read (on success or failure)
+            std::lock_guard<std::mutex> lk(p->mu);
+            x.stage_pending = false;
+            x.reads = nullptr;
+            p->cv.notify_all();
+        }
         if (rc) return rc;
     } else if (x.mode == PipeMode::COPY) {
         x.resident = false;
@@ -253,6 +267,7 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
     x->cols = nuclseq_columns != 0;
     x->mode = mode;
     x->reads = mode == PipeMode::DEFER ? reads : nullptr;
+    x->stage_pending = mode == PipeMode::DEFER;
     x->view = nullptr;
     drop_cols(*x);
     for (double &t : x->t) t = 0;
@@ -261,6 +276,18 @@ int pipeline_submit_ex(bsq_pipeline *p, const bsq_opts *opts, const void *const 
     x->state = SlotState::QUEUED;
     ++p->n_submit;
     p->cv.notify_all();
+    return BSQ_OK;
+}
+
+int pipeline_wait_staged(bsq_pipeline *p, int64_t upto)
+{
+    if (!p) return fail(BSQ_E_INVALID, "invalid argument");
+    std::unique_lock<std::mutex> lk(p->mu);
+    p->cv.wait(lk, [&] {
+        for (auto &x : p->s)
+            if (x->stage_pending && (int64_t)x->job < upto) return false;
+        return true;
+    });
     return BSQ_OK;
 }
 
@@ -369,6 +396,21 @@ extern "C" int bsq_pipeline_submit(bsq_pipeline *p, const bsq_opts *opts, const 
 {
     return pipeline_submit_ex(p, opts, reads, n_reads, first_call_seq, nuclseq_columns, PipeMode::COPY);
 }
+
+extern "C" int bsq_pipeline_submit_deferred(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                                            uint64_t first_call_seq, int nuclseq_columns, int64_t *job)
+{
+    uint64_t j = 0;
+    if (p) {
+        std::lock_guard<std::mutex> lk(p->mu);
+        j = p->n_submit;
+    }
+    const int rc = pipeline_submit_ex(p, opts, reads, n_reads, first_call_seq, nuclseq_columns, PipeMode::DEFER);
+    if (!rc && job) *job = (int64_t)j;
+    return rc;
+}
+
+extern "C" int bsq_pipeline_wait_staged(bsq_pipeline *p, int64_t upto) { return pipeline_wait_staged(p, upto); }
 
 extern "C" int bsq_pipeline_next(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off)
 {

@@ -128,9 +128,10 @@ void BwaIndex::ensure_group() const
     group_ = g;
 }
 
-void BwaIndex::submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
-                           const BsqMemOpt *opts) const
+int64_t BwaIndex::submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
+                              const BsqMemOpt *opts, bool deferred) const
 {
+    int64_t ticket = -1;
     if ((int)pending_.size() + held_ >= pipeline_depth())
         throw BsqFailure(BSQ_E_INVALID, "every pipeline slot holds a fetch (take and release the oldest first)");
     Pending pd;
@@ -139,7 +140,7 @@ void BwaIndex::submit_rows(const NucleotideSequence *const *seqs, int32_t n, boo
     if (n <= 0 || empty()) {   // bwa.cpp:142-143: no mem_align1 call, no lrand48 value drawn
         pd.empty = true;
         pending_.push_back(pd);
-        return;
+        return ticket;
     }
     const void *const *ptrs = reinterpret_cast<const void *const *>(seqs);
     const bsq_opts o = (opts ? *opts : *options).c_abi();
@@ -161,11 +162,18 @@ void BwaIndex::submit_rows(const NucleotideSequence *const *seqs, int32_t n, boo
         }
     } else {
         ensure_pipe();
-        check(bsq_pipeline_submit(pipe_, &o, ptrs, n, calls, nuclseq_columns ? 1 : 0));
+        if (deferred) check(bsq_pipeline_submit_deferred(pipe_, &o, ptrs, n, calls, nuclseq_columns ? 1 : 0, &ticket));
+        else check(bsq_pipeline_submit(pipe_, &o, ptrs, n, calls, nuclseq_columns ? 1 : 0));
         ++in_pipe_;
     }
     calls += (uint64_t)n;
     pending_.push_back(pd);
+    return ticket;
+}
+
+void BwaIndex::wait_staged(int64_t ticket) const
+{
+    if (ticket >= 0 && pipe_) check(bsq_pipeline_wait_staged(pipe_, ticket + 1));
 }
 
 const BwaRows &BwaIndex::take_rows() const

@@ -113,8 +113,13 @@ public:
     // take_rows waits for the oldest submitted fetch and lends its rows until release_rows.  At most
     // pipeline_depth() fetches may be submitted and not released.  Rows come back in submission order, with
     // lrand48 positions as if aligned one after another.  Not for concurrent use by several threads.
-    void submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
-                     const BsqMemOpt *opts = nullptr) const;
+    // deferred = true: the fetch is staged by a pipeline worker instead of on this thread; `seqs` and the values
+    // they point to must then stay valid until wait_staged() has passed the returned ticket (group and empty fetches
+    // are done at submit and return ticket -1).
+    int64_t submit_rows(const NucleotideSequence *const *seqs, int32_t n, bool nuclseq_columns,
+                        const BsqMemOpt *opts = nullptr, bool deferred = false) const;
+    // every deferred fetch up to and including `ticket` has been staged (its tuples may be freed)
+    void wait_staged(int64_t ticket) const;
     const BwaRows &take_rows() const;
     void release_rows() const;
     int pipeline_depth() const;

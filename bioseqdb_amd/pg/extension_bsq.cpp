@@ -139,14 +139,34 @@ constexpr long kRefFetchRows = 64;   // reference rows are long; their bytes are
 // iterate_nuclseq_table (extension.cpp:156-195): (int2/4/8 id, nuclseq) rows of `sql`, NULL rows skipped,
 // the column types checked on every fetch with the reference's messages.  Each fetch of up to `fetch` rows is
 // handed to on_rows(ids, seqs) while its tuples are valid, then released.
-template <class F>
-void for_each_fetch(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows)
+// If on_rows returns a ticket >= 0 (a deferred pipeline submission that still reads the tuples), the tuples of that
+// fetch are freed only after the NEXT fetch has been fetched and handed over and wait(ticket) has returned, so the
+// staging of fetch k runs on a pipeline worker while this backend fetches k+1.  Unwinding with a ticket
+// outstanding waits for it first: no worker reads tuple memory after control leaves this function.
+template <class F, class W>
+void for_each_fetch_held(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows, W &&wait)
 {
     Portal portal = nullptr;
     pg_call([&] { portal = SPI_cursor_open_with_args(nullptr, sql, 0, nullptr, nullptr, nullptr, true, 0); });
-    std::vector<int64_t> ids;
-    std::vector<const NucleotideSequence *> seqs;
-    for (;;) {
+    std::vector<int64_t> ids[2];
+    std::vector<const NucleotideSequence *> seqs[2];   // alternate: the held fetch's pointers stay valid
+    SPITupleTable *held_tt = nullptr;
+    int64_t held_ticket = -1;
+    struct Guard {
+        W &wait;
+        int64_t &ticket;
+        ~Guard()
+        {
+            if (ticket >= 0) {
+                try { wait(ticket); } catch (...) {}
+            }
+        }
+    } guard{wait, held_ticket};
+    auto release_held = [&] {
+        if (held_ticket >= 0) { const int64_t t = held_ticket; held_ticket = -1; wait(t); }
+        if (held_tt) { SPITupleTable *t = held_tt; held_tt = nullptr; pg_call([&] { SPI_freetuptable(t); }); }
+    };
+    for (int cur = 0;; cur ^= 1) {
         uint64 n = 0;
         SPITupleTable *tt = nullptr;
         pg_call([&] {
@@ -164,8 +184,10 @@ void for_each_fetch(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows)
         if (id_type != INT2OID && id_type != INT4OID && id_type != INT8OID)
             throw SqlError{ERRCODE_DATATYPE_MISMATCH, "expected column of integers"};
         if (seq_type != nuclseq_oid) throw SqlError{ERRCODE_DATATYPE_MISMATCH, "expected column of nuclseqs"};
-        ids.resize((size_t)n);
-        seqs.resize((size_t)n);
+        std::vector<int64_t> &id_v = ids[cur];
+        std::vector<const NucleotideSequence *> &seq_v = seqs[cur];
+        id_v.resize((size_t)n);
+        seq_v.resize((size_t)n);
         size_t kept = 0;
         pg_call([&] {
             for (uint64 i = 0; i < n; ++i) {
@@ -173,18 +195,32 @@ void for_each_fetch(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows)
                 const Datum id = SPI_getbinval(tt->vals[i], tt->tupdesc, 1, &null_id);
                 const Datum seq = SPI_getbinval(tt->vals[i], tt->tupdesc, 2, &null_seq);
                 if (null_id || null_seq) continue;
-                ids[kept] = id_type == INT2OID ? (int64_t)DatumGetInt16(id)
-                            : id_type == INT4OID ? (int64_t)DatumGetInt32(id) : (int64_t)DatumGetInt64(id);
-                seqs[kept] = reinterpret_cast<const NucleotideSequence *>(PG_DETOAST_DATUM(seq));
+                id_v[kept] = id_type == INT2OID ? (int64_t)DatumGetInt16(id)
+                             : id_type == INT4OID ? (int64_t)DatumGetInt32(id) : (int64_t)DatumGetInt64(id);
+                seq_v[kept] = reinterpret_cast<const NucleotideSequence *>(PG_DETOAST_DATUM(seq));
                 ++kept;
             }
         });
-        ids.resize(kept);
-        seqs.resize(kept);
-        on_rows(ids, seqs);
-        pg_call([&] { SPI_freetuptable(tt); });
+        id_v.resize(kept);
+        seq_v.resize(kept);
+        const int64_t ticket = on_rows(id_v, seq_v);
+        release_held();   // the previous fetch: staged by now or waited for
+        if (ticket >= 0) { held_tt = tt; held_ticket = ticket; }
+        else pg_call([&] { SPI_freetuptable(tt); });
     }
+    release_held();
     pg_call([&] { SPI_cursor_close(portal); });
+}
+
+template <class F>
+void for_each_fetch(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows)
+{
+    for_each_fetch_held(sql, nuclseq_oid, fetch,
+                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
+                            on_rows(ids, seqs);
+                            return (int64_t)-1;
+                        },
+                        [](int64_t) {});
 }
 
 // ---- options and index ---------------------------------------------------------------------------------
@@ -398,13 +434,18 @@ void multi_search(FunctionCallInfo fcinfo)
         index.release_rows();
         ids_q.pop_front();
     };
-    for_each_fetch(query_sql, nuclseq_oid, query_fetch_rows(),
-                   [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
-                       if ((int)ids_q.size() >= depth) drain_one();
-                       index.submit_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt);
-                       ids_q.push_back(ids);
-                       st.reads += (long long)seqs.size();
-                   });
+    // Each fetch is staged by a pipeline worker (deferred submission) while this backend fetches the next one; its
+    // tuples are freed once that staging is done (for_each_fetch_held).
+    for_each_fetch_held(query_sql, nuclseq_oid, query_fetch_rows(),
+                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
+                            if ((int)ids_q.size() >= depth) drain_one();
+                            const int64_t ticket =
+                                index.submit_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt, true);
+                            ids_q.push_back(ids);
+                            st.reads += (long long)seqs.size();
+                            return ticket;
+                        },
+                        [&](int64_t ticket) { index.wait_staged(ticket); });
     while (!ids_q.empty()) drain_one();
     st.align_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     finish(rsi, store, desc, "nuclseq_multi_search_bwa", ci, st);

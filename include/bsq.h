@@ -259,6 +259,14 @@ void bsq_pipeline_free(bsq_pipeline *p);
 int bsq_pipeline_slots(const bsq_pipeline *p);
 int bsq_pipeline_submit(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
                         uint64_t first_call_seq, int nuclseq_columns);
+/* As bsq_pipeline_submit, but the fetch is staged by the slot's worker thread instead of the caller's: `reads` and
+ * the varlenas they point to must stay valid until bsq_pipeline_wait_staged(p, k) returns for some k > *job (the
+ * submission's number, counted from the pipeline's creation).  A backend frees fetch k's tuples after fetching k+1
+ * and waiting for k's staging, so the staging overlaps its own SPI work (extension.cpp:156-195's fetch loop). */
+int bsq_pipeline_submit_deferred(bsq_pipeline *p, const bsq_opts *opts, const void *const *reads, int32_t n_reads,
+                                 uint64_t first_call_seq, int nuclseq_columns, int64_t *job);
+/* Returns once no deferred submission numbered < upto still reads its caller's varlenas. */
+int bsq_pipeline_wait_staged(bsq_pipeline *p, int64_t upto);
 int bsq_pipeline_next(bsq_pipeline *p, const bsq_hits **view, const uint8_t **cols, const int64_t **col_off);
 int bsq_pipeline_release(bsq_pipeline *p);
 

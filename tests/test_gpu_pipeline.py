@@ -117,6 +117,66 @@ def test_pipeline_fetches_equal_single_calls(setup, slots):
             assert cols == _columns(L, pi.handle, pi.options, fs, 500 + first), first
 
 
+@pytest.mark.parametrize("slots", [2, 4])
+def test_deferred_staging_fetches_equal_single_calls(setup, slots):
+    """bsq_pipeline_submit_deferred (the drop-in's cursor loop since round 5, extension_bsq.cpp for_each_fetch_held):
+    fetch k is staged by a pipeline worker; the caller frees its varlenas (here: overwrites them with other reads)
+    only after submitting fetch k+1 and bsq_pipeline_wait_staged past k's ticket.  Every fetch's rows and columns
+    equal aligning it alone, tickets count submissions, and a fetch freed after its wait cannot change its rows."""
+    pi, seqs = setup
+    L = N.lib()
+    sizes = [4000, 1, 0, 6000, 333, 5000, 2]
+    fetches, lo = [], 0
+    for s in sizes:
+        fetches.append((lo, seqs[lo:lo + s]))
+        lo += s
+    junk = seqs[-1].raw
+    p = ctypes.c_void_p()
+    N.check(L.bsq_pipeline_create(pi.handle, slots, ctypes.byref(p)))
+    try:
+        pending, got, held = [], [], None
+
+        def take():
+            v = ctypes.POINTER(N.Hits)()
+            c = ctypes.c_void_p()
+            o = ctypes.POINTER(ctypes.c_int64)()
+            N.check(L.bsq_pipeline_next(p, ctypes.byref(v), ctypes.byref(c), ctypes.byref(o)))
+            first, n = pending.pop(0)
+            nh = v.contents.n_hits
+            got.append((first, n, _records(v.contents, n), ctypes.string_at(c, o[2 * nh]) if nh else b""))
+            N.check(L.bsq_pipeline_release(p))
+
+        def free(h):   # "SPI_freetuptable": the buffers now hold another read's bytes
+            ticket, bufs, _ptrs = h
+            N.check(L.bsq_pipeline_wait_staged(p, ticket + 1))
+            for b in bufs:
+                ctypes.memmove(b, junk, min(len(junk), ctypes.sizeof(b)))
+
+        for k, (first, fs) in enumerate(fetches):
+            if len(pending) == slots:
+                take()
+            bufs = [ctypes.create_string_buffer(s.raw, len(s.raw)) for s in fs]
+            ptrs = (ctypes.c_void_p * max(len(fs), 1))(*[ctypes.addressof(b) for b in bufs])
+            tk = ctypes.c_int64(-7)
+            N.check(L.bsq_pipeline_submit_deferred(p, ctypes.byref(pi.options), ptrs, len(fs), 900 + first, 1,
+                                                   ctypes.byref(tk)))
+            assert tk.value == k   # tickets number the submissions
+            if held is not None:
+                free(held)
+            held = (tk.value, bufs, ptrs)   # the pointer array is read by the worker too
+            pending.append((first, len(fs)))
+        free(held)
+        while pending:
+            take()
+    finally:
+        L.bsq_pipeline_free(p)
+    assert [g[0] for g in got] == [f[0] for f in fetches]
+    for (first, fs), (_, n, rec, cols) in zip(fetches, got):
+        assert rec == _one_shot(L, pi.handle, pi.options, fs, 900 + first), first
+        if fs:
+            assert cols == _columns(L, pi.handle, pi.options, fs, 900 + first), first
+
+
 def test_pipeline_full_and_empty(setup):
     pi, seqs = setup
     L = N.lib()
