@@ -515,7 +515,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
 
 template <typename X, typename Z, typename Q>
 DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int max_intv, Intv &mem,
-                         uint64_t &nblk, uint64_t &nkm)
+                         uint64_t &nblk, uint64_t &nkm, bool walk)
 {
     mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
     if (q[x] > 3) return x + 1;
@@ -543,6 +543,27 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int 
     }
     int qi = i0 < len ? q[i0] : 0;
     for (int i = i0; i < len; ++i) {
+        if (ik2 == 1 && max_intv > 1 && walk) {
+            // A unique interval stays [x0, x0] while the string follows its one occurrence (at SA[x0] in T) and
+            // is empty from the first differing base on; an empty one stays empty.  Sizes stay below max_intv, so
+            // the loop returns at the first step j >= x + min_len (or at a hole, or runs off the read): decide that
+            // step from the text instead of one bwt_extend per base.  The seed's x[1] is not tracked on this path
+            // (mem_chain reads x[0], x[2] and info only -- the same convention as the SMEM list entries).
+            const int js = i > x + min_len ? i : x + min_len;
+            const int jend = js < len ? js : len - 1;
+            int h = i;
+            while (h <= jend && q[h] < 4) ++h;
+            if (h <= jend) return h + 1;          // a hole ends the call
+            if (js >= len) return len;            // the read ends first: no seed
+            const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
+            bool match = true;
+            for (int j = i; j <= js && match; ++j) match = p + j < nT && q[j] == fm.tbase(p + j);
+            if (match) {
+                mem.x[0] = ik0; mem.x[1] = 0; mem.x[2] = 1;
+                mem.info = (uint64_t)x << 32 | (uint64_t)(js + 1);
+            }
+            return js + 1;
+        }
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;
         if (cur < 4) {
@@ -675,7 +696,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             while (x < len && !ovf) {
                 if (q[x] < 4) {
                     Intv m;
-                    x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm);
+                    x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm, o.ss_walk != 0);
                     if (m.x[2] > 0) {
                         if (S.n >= S.cap) { ovf = true; break; }
                         Intv &d = S.a[S.n++];
@@ -708,6 +729,141 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
     wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
 }
 
+// k_smem_lanes: k_smem_lds with persistent lanes that step through their reads one CALL at a time.
+// In k_smem_lds a lane owns one read, and the wave runs pass 1 (bwt_smem1 over x), pass 2 (re-seeding) and pass 3
+// (bwt_seed_strategy1) as three loops: a lane whose read needs 2 bwt_smem1 calls idles while another lane of the wave
+// makes 10 (the 2 % random reads make ~10 short SMEMs), and the wave ends with its slowest read.  Here each trip of
+// the outer loop makes at most one call per lane -- one bwt_smem1 (pass 1 or 2: both lanes' kinds share the one call
+// site) or one bwt_seed_strategy1 -- after an ALU-only step that moves each lane to its next call (holes skipped,
+// pass-2 entries that do not qualify skipped, pass changes); a lane that has finished its read sorts its intervals
+// and takes the next read (li += the grid's lanes; lane = li % 64, so the wave-transposed codes and the per-wave
+// slots keep their layouts).  Per read the calls, their order and their arguments are k_smem_lds's: identical intervals.
+template <typename X, typename Z, typename Q>
+__global__ void __launch_bounds__(64) k_smem_lanes(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
+                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
+{
+    const int t = threadIdx.x;
+    LList<X, Z> L;   // LDS: [x0: 64*lcap X][x2: 64*lcap Z][end: 64*lcap u16]
+    L.x0 = t;
+    L.x2 = (int)((size_t)64 * lcap * sizeof(X) / sizeof(Z)) + t;
+    L.end = (int)((size_t)64 * lcap * (sizeof(X) + sizeof(Z)) / 2) + t;
+    L.stride = 64;
+    L.cap = lcap;
+    L.gcap = spill ? gcap : 0;
+    const size_t spill_tot = (size_t)(n + 63) / 64 * 64 * (size_t)gcap;
+    FM<X> fm;
+    fm.occ = ix.occ;
+    fm.occ32 = ix.occ32;
+    fm.sup = ix.sup;
+    fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
+    fm.primary = (X)ix.primary;
+    fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
+    fm.K = ix.kmer_k;
+    fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
+    const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
+    const int lstride = gridDim.x * 64;
+    uint64_t nblk = 0, nkm = 0;
+    enum { NEXT, P1, P2, P3, FIN, DONE };
+    int st = NEXT, li = blockIdx.x * 64 + t - lstride, len = 0, x = 0, k2 = 0, old_n = 0;
+    bool ovf = false;
+    Q q{};
+    OutSlot S{SP<Intv>{intv_out}, 0, cp.intv, 0};
+    for (;;) {
+        if (st == NEXT) {   // the lane's next read
+            li += lstride;
+            if (li >= n) st = DONE;
+            else {
+                const size_t me = ((size_t)li >> 6) * 64 * (size_t)gcap + ((size_t)li & 63);
+                L.gx0 = reinterpret_cast<X *>(spill) + me;
+                L.gx2 = reinterpret_cast<Z *>(spill + spill_tot * sizeof(X)) + me;
+                L.gend = reinterpret_cast<uint32_t *>(spill + spill_tot * (sizeof(X) + sizeof(Z))) + me;
+                if constexpr (__is_same(Q, QT)) q = QT{codes + (size_t)(li >> 6) * 64 * (size_t)qcap + (li & 63)};
+                else q = codes + offs[li];
+                len = (int)(offs[li + 1] - offs[li]);
+                ovf = false;
+                S = OutSlot{SP<Intv>{intv_out + intv_slot_at_d(li, 0, cp.intv)}, 0, cp.intv, 0};
+                x = 0;
+                st = P1;
+            }
+        }
+        if (__ballot(st != DONE) == 0) break;
+        // to the lane's next call (ALU and the read's bases only)
+        int sx = 0, mi = 1;
+        bool call_smem = false, call_ss = false;
+        for (bool adv = st == P1 || st == P2 || st == P3; adv;) {
+            adv = false;
+            if (st == P1) {
+                while (x < len && q[x] > 3) ++x;
+                if (x < len && !ovf) { call_smem = true; sx = x; mi = 1; }
+                else { old_n = S.n; k2 = 0; st = P2; adv = true; }
+            } else if (st == P2) {
+                if (ovf || k2 >= old_n) { st = P3; x = 0; adv = true; }
+                else {
+                    const Intv p = S.a[k2];
+                    const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
+                    if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) { ++k2; adv = true; }
+                    else { call_smem = true; sx = (start + end) >> 1; mi = (int)p.x[2] + 1; }
+                }
+            } else if (st == P3) {
+                if (o.max_mem_intv <= 0 || ovf) st = FIN;
+                else {
+                    while (x < len && q[x] > 3) ++x;
+                    if (x < len) call_ss = true;
+                    else st = FIN;
+                }
+            }
+        }
+        if (call_smem) {   // pass 1 and pass 2 share this call site
+            const int r = smem1_lds(fm, len, q, sx, mi, L, S, ovf, nblk, nkm);
+            if (!ovf) {   // take_mem1
+                const bool pass2 = st == P2;
+                for (int k = 0; k < S.n1; ++k) {
+                    const Intv &m = S.a[S.cap - S.n1 + k];
+                    const uint64_t m0 = m.x[0], m2 = m.x[2], mn = m.info;
+                    const uint32_t s0 = (uint32_t)(mn >> 32), en = (uint32_t)mn;
+                    const bool keep = pass2 ? (uint64_t)(en - s0) >= (uint64_t)o.min_seed_len : (int)(en - s0) >= o.min_seed_len;
+                    if (keep) { Intv &d = S.a[S.n++]; d.x[0] = m0; d.x[1] = 0; d.x[2] = m2; d.info = mn; }
+                }
+                S.n1 = 0;
+            }
+            if (st == P1) x = r;
+            else ++k2;
+        }
+        if (call_ss) {
+            Intv m;
+            x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm, o.ss_walk != 0);
+            if (m.x[2] > 0) {
+                if (S.n >= S.cap) ovf = true;
+                else { Intv &d = S.a[S.n++]; d.x[0] = m.x[0]; d.x[1] = m.x[1]; d.x[2] = m.x[2]; d.info = m.info; }
+            }
+        }
+        if (st == FIN) {
+            if (ovf) {
+                status[li] |= ST_OVERFLOW;
+                n_intv[li] = 0;
+            } else {
+                const SP<Intv> out = S.a;
+                for (int a = 1; a < S.n; ++a) {   // equal keys are identical intervals: any correct sort is exact
+                    const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
+                    int b = a;
+                    for (; b > 0; --b) {
+                        const uint64_t pi = out[b - 1].info;
+                        if (!(ti < pi)) break;
+                        out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
+                        out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
+                    }
+                    out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
+                }
+                n_intv[li] = S.n;
+            }
+            st = NEXT;
+        }
+    }
+    wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
+    wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
+}
+
 // LDS bytes per thread for `lcap` list entries
 template <typename X, typename Z>
 static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (sizeof(X) + sizeof(Z) + 2); }
@@ -731,35 +887,41 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int T = 64;
     int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
+    // persistent lanes (k_smem_lanes, BSQ_SMEM_LANES=0: k_smem_lds): each lane steps through rpl reads call by call
+    const char *le = getenv("BSQ_SMEM_LANES");
+    const bool lanes = !(le && *le == '0');
+    if (lanes) {
+        const char *r = getenv("BSQ_SMEM_RPL");
+        const int rpl = r && atoi(r) > 0 ? atoi(r) : 4;
+        grid = (grid + rpl - 1) / rpl;
+    }
     if (const char *g = getenv("BSQ_SMEM_GRID")) { const int c = atoi(g); if (c > 0 && c < grid) grid = c; }
     const int L = cp.max_len;
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
-    if (!ix.wide) {
-        size_t sh = lds_bytes<uint32_t, uint32_t>(T, lcap);
-        if (codes_t)
-            hipLaunchKernelGGL((k_smem_lds<uint32_t, uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
-                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
-        else
-            hipLaunchKernelGGL((k_smem_lds<uint32_t, uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
-                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
-    } else if (wide_z32(ix)) {   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
-        size_t sh = lds_bytes<uint64_t, uint32_t>(T, lcap);
-        if (codes_t)
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint32_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
-                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
-        else
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint32_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
-                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
-    } else {
-        size_t sh = lds_bytes<uint64_t, uint64_t>(T, lcap);
-        if (codes_t)
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint64_t, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,
-                               intv, n_intv, status, ctr, lcap, spill, gcap, L);
-        else
-            hipLaunchKernelGGL((k_smem_lds<uint64_t, uint64_t, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,
-                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);
-    }
+#define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
+    do {                                                                                                               \
+        const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
+        if (lanes) {                                                                                                   \
+            if (codes_t)                                                                                               \
+                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, \
+                                   intv, n_intv, status, ctr, lcap, spill, gcap, L);                                    \
+            else                                                                                                       \
+                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp,     \
+                                   codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
+        } else {                                                                                                       \
+            if (codes_t)                                                                                               \
+                hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,   \
+                                   intv, n_intv, status, ctr, lcap, spill, gcap, L);                                    \
+            else                                                                                                       \
+                hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp,       \
+                                   codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
+        }                                                                                                              \
+    } while (0)
+    if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t);
+    else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
+    else BSQ_SMEM_LAUNCH(uint64_t, uint64_t);
+#undef BSQ_SMEM_LAUNCH
     return hipGetLastError();
 }
 

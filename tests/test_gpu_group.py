@@ -153,3 +153,31 @@ def test_group_errors():
         assert rc == N.BSQ_E_INVALID and b"replicate" in L.bsq_last_error()
     finally:
         L.bsq_group_free(g)
+
+
+def test_group_two_distinct_devices_routes_agree(setup):
+    """on a node with 2+ GPUs, a group over two distinct devices (RCCL broadcast of the tables, a member on
+    each device) gives byte-identical records over both exchange routes -- every member's own link (LINKS) and peer
+    DMA over xGMI into member 0 first (VIA_FIRST, the cross-device event wait and peer-access path of relay_records)
+    -- and equal to one device.  Skipped on a one-GPU box."""
+    L = N.lib()
+    if L.bsq_device_count() < 2:
+        pytest.skip("needs two HIP devices")
+    pi, _, seqs = setup
+    n = len(seqs)
+    ptrs = (ctypes.c_void_p * n)(*[s.ptr for s in seqs])
+    want = _one_device(L, pi.handle, pi.options, ptrs, n, 77)
+    g = ctypes.c_void_p()
+    N.check(L.bsq_group_create((ctypes.c_int * 2)(0, 1), 2, ctypes.byref(g)))
+    try:
+        N.check(L.bsq_group_replicate(g, pi.handle, None))
+        got = []
+        for mode in (0, 1, 0):
+            N.check(L.bsq_group_set_exchange(g, mode))
+            N.check(L.bsq_group_run(g, ctypes.byref(pi.options), ptrs, n, 77))
+            got.append(_records(L.bsq_group_hits(g).contents, n))
+            N.check(L.bsq_group_run_rounds(g, ctypes.byref(pi.options), n, 77, 2))
+            got.append(_records(L.bsq_group_hits(g).contents, n))
+        assert all(r == want for r in got)
+    finally:
+        L.bsq_group_free(g)
