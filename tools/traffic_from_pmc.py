@@ -11,7 +11,7 @@ Usage: traffic_from_pmc.py <profile dir> <out json> <round tag>
 import csv, glob, json, os, sys
 
 # stage -> kernels its HIP events bracket (the sorts' rocprim kernels are negligible and not counted)
-KERNELS = {"smem": ["k_codes_wave", "k_smem_lds<", "k_smem_sm", "k_pack_reads", "k_intv_sort"], "chain": ["k_chain_s", "k_chain<"],
+KERNELS = {"smem": ["k_codes_wave", "k_smem_lds<", "k_smem_lanes<", "k_smem_sm", "k_pack_reads", "k_intv_sort"], "chain": ["k_chain_s", "k_chain<"],
            "extend": ["k_ext_key", "k_extend<"],
            "reg2aln": ["k_r2a_key", "k_reg2aln_diag", "k_reg2aln_g<16>", "k_reg2aln_g<32>", "bsq::k_reg2aln_w"]}
 
