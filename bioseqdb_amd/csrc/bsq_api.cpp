@@ -865,7 +865,7 @@ DOpts make_dopts(const bsq_opts &o)
     d.max_mem_intv = 20; d.split_factor = 1.5f; d.mask_level = 0.50f; d.drop_ratio = 0.50f; d.mask_level_redun = 0.95f;
     // mem_opt_init fills mat with a=1, b=4 and bioseqdb never refills it (Q2)
     d.mat_match = 1; d.mat_mismatch = -4; d.mat_amb = -1; d.mat_max = 1;
-    { const char *e = getenv("BSQ_SS_WALK"); d.ss_walk = !(e && *e == '0'); }
+    { const char *e = getenv("BSQ_SS_WALK"); d.ss_walk = e && *e == '1'; }
     return d;
 }
 

@@ -116,9 +116,10 @@ class Core {
         std::vector<double> wait((size_t)L, 0.0);
         std::vector<std::string> lane_err((size_t)L);
         auto batch = [&](int i) {
+            bool resume_failed = false;   // the next round publishes a failure instead of running
             for (int k = 0; k < rounds; ++k) {
                 Records rec;
-                const int st = produce(i, k, rec);
+                const int st = resume_failed ? -3 : produce(i, k, rec);
                 const auto t0 = std::chrono::steady_clock::now();
                 std::unique_lock<std::mutex> lk(mu);
                 if (stop) return;
@@ -131,10 +132,11 @@ class Core {
                 if (stop) return;
                 lk.unlock();
                 std::string e;
-                if (t_.batch_resume(i, e)) {   // a local transport error: the exchange thread will stop too
+                if (t_.batch_resume(i, e)) {   // a local transport error: carried to every rank by the next header
                     lk.lock();
                     if (lane_err[(size_t)i].empty()) lane_err[(size_t)i] = e;
-                    return;
+                    lk.unlock();
+                    resume_failed = true;
                 }
             }
         };

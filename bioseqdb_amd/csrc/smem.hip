@@ -887,9 +887,9 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int T = 64;
     int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
-    // persistent lanes (k_smem_lanes, BSQ_SMEM_LANES=0: k_smem_lds): each lane steps through rpl reads call by call
+    // persistent lanes (k_smem_lanes, BSQ_SMEM_LANES=1; default k_smem_lds): each lane steps through rpl reads call by call
     const char *le = getenv("BSQ_SMEM_LANES");
-    const bool lanes = !(le && *le == '0');
+    const bool lanes = le && *le == '1';
     if (lanes) {
         const char *r = getenv("BSQ_SMEM_RPL");
         const int rpl = r && atoi(r) > 0 ? atoi(r) : 4;
