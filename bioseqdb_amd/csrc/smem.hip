@@ -514,6 +514,225 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
 }
 
 template <typename X, typename Z, typename Q>
+DEV int smem1_merged(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S,
+                  bool &ovf, uint64_t &nblk, uint64_t &nkm)
+{
+    S.n1 = 0;
+    if (q[x] > 3) return x + 1;
+    if (min_intv < 1) min_intv = 1;
+    int c0 = q[x];
+    X ik0 = fm.L2(c0) + 1, ik1 = fm.L2(3 - c0) + 1;
+    Z ik2 = (Z)(fm.L2(c0 + 1) - fm.L2(c0));
+    int ikend = x + 1;
+    int n = 0, i = x + 1;
+    uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
+    bool stop = false;               // the forward walk ended early (hole or interval below min_intv)
+    {
+        // Lengths 2..min(K, len - x) come from the k-mer table.  Their table rows depend only on the read's
+        // bases, so every row is loaded before the first one is used (one round trip instead of K - 1);
+        // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
+        // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
+        // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
+        constexpr int KM = 11;   // kmer_depth() never exceeds 11
+        const int Lt = fm.K < len - x ? fm.K : len - x;
+        int cb[KM + 1];
+#pragma unroll
+        for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
+        X e0[KM + 1];
+        Z e2[KM + 1];
+        int nt = 1;   // bases from x covered without a hole (capped at Lt)
+#pragma unroll
+        for (int t = 2; t <= KM; ++t) {
+            if (nt == t - 1 && cb[t] < 4) {
+                fcode = fcode << 2 | (uint32_t)cb[t];
+                fm.kget02(koff(t) + fcode, e0[t], e2[t]);
+                nt = t;
+            }
+        }
+        if (nt >= 2) {
+            nkm += (uint64_t)(nt - 1);
+            const X x1_last = fm.kget1(koff(nt) + fcode);
+#pragma unroll
+            for (int t = 2; t <= KM; ++t) {
+                if (t <= nt && !stop) {
+                    const X n0 = e0[t];
+                    const Z n2 = e2[t];
+                    if (n2 != ik2) {
+                        if (n >= L.total()) { ovf = true; return len; }
+                        L.set(n++, ik0, ik2, ikend);
+                        if (n2 < (Z)min_intv) { stop = true; i = x + t - 1; }
+                    }
+                    if (!stop) { ik0 = n0; ik2 = n2; ikend = x + t; }
+                }
+            }
+            ik1 = x1_last;
+        }
+        if (!stop) {
+            i = x + nt;
+            if (nt < Lt) {   // q[x + nt] is a hole: the walk stops there
+                if (n >= L.total()) { ovf = true; return len; }
+                L.set(n++, ik0, ik2, ikend);
+                stop = true;
+            }
+        }
+    }
+    int qi = !stop && i < len ? q[i] : 0;
+    // One loop for both phases of bwt_smem1: a lane that has finished its forward walk (reversed its list and set up
+    // the backward pass) takes its backward pairs in the same trips in which other lanes of the wave still extend
+    // forward, instead of waiting at the forward loop's exit for the wave's longest forward walk.  Per lane every
+    // step, and the order of the steps, is smem1_lds's.
+    const int K = fm.K;
+    int phase = 0;   // 0 forward, 1 backward, 2 done
+    int ret = 0, last_start = 0x7fffffff, c = -1, nc = 0, j = 0;
+    uint32_t wcode = 0;
+    Z last_x2 = 0;
+    for (;;) {
+        if (phase == 0) {
+            bool fend = stop || i >= len;
+            if (!fend) {
+                if (ik2 == 1 && min_intv <= 1) {   // the unique-interval text walk (smem1_lds)
+                    const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
+                    int k = i;
+                    for (;;) {
+                        constexpr int W = 8;
+                        int qc[W], tc[W];
+#pragma unroll
+                        for (int t = 0; t < W; ++t) {
+                            const bool in = k + t < len && p + k + t < nT;
+                            qc[t] = in ? q[k + t] : 5;
+                            tc[t] = in ? fm.tbase(p + k + t) : 4;
+                        }
+                        int r = W;
+#pragma unroll
+                        for (int t = W - 1; t >= 0; --t)
+                            if (qc[t] != tc[t]) r = t;
+                        k += r;
+                        if (r < W) break;
+                    }
+                    ikend = k;
+                    i = k;
+                    if (k < len) {
+                        if (n >= L.total()) { ovf = true; return len; }
+                        L.set(n++, ik0, ik2, ikend);
+                    }
+                    fend = true;
+                } else {
+                    const int cur = qi;
+                    qi = i + 1 < len ? q[i + 1] : 0;
+                    if (cur < 4) {
+                        const int cc = 3 - cur;
+                        X n1, n0;
+                        Z n2;
+                        fcode = fcode << 2 | (uint32_t)cur;
+                        if (i - x + 1 <= fm.K) {
+                            fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
+                            ++nkm;
+                        } else extend1(fm, ik1, ik0, ik2, cc, n1, n0, n2, nblk);
+                        if (n2 != ik2) {
+                            if (n >= L.total()) { ovf = true; return len; }
+                            L.set(n++, ik0, ik2, ikend);
+                            if (n2 < (Z)min_intv) fend = true;
+                        }
+                        if (!fend) {
+                            ik0 = n0; ik1 = n1; ik2 = n2; ikend = i + 1;
+                            if (++i >= len) fend = true;
+                        }
+                    } else {
+                        if (n >= L.total()) { ovf = true; return len; }
+                        L.set(n++, ik0, ik2, ikend);
+                        fend = true;
+                    }
+                }
+            }
+            if (fend) {   // the forward walk is over: last push, reversal, backward set-up
+                if (i == len) {
+                    if (n >= L.total()) { ovf = true; return len; }
+                    L.set(n++, ik0, ik2, ikend);
+                }
+                for (int jj = 0; jj < (n >> 1); ++jj) {
+                    X a0, b0;
+                    Z a2, b2;
+                    int ae, be;
+                    L.get(jj, a0, a2, ae);
+                    L.get(n - 1 - jj, b0, b2, be);
+                    L.set(jj, b0, b2, be);
+                    L.set(n - 1 - jj, a0, a2, ae);
+                }
+                { X d0; Z d2; L.get(0, d0, d2, ret); }
+                for (int t = 0; t < K; ++t) wcode = wcode << 2 | (x + t < len ? (uint32_t)(q[x + t] & 3) : 0u);
+                i = x - 1;
+                c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+                if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
+                phase = 1;
+            }
+        }
+        if (phase == 1) {   // one pair of the flat backward loop (smem1_lds)
+            const bool hb = j + 1 < n;
+            X pa0, pb0;
+            Z pa2, pb2;
+            int pae, pbe;
+            L.get(j, pa0, pa2, pae);
+            L.get(hb ? j + 1 : j, pb0, pb2, pbe);
+            X oa0 = 0, ob0 = 0;
+            Z oa2 = 0, ob2 = 0;
+            if (c >= 0) {
+                const int La = pae - i, Lb = pbe - i;
+                const bool ta = La <= K, tb = hb && Lb <= K;
+                X ea0 = 0, eb0 = 0;
+                Z ea2 = 0, eb2 = 0;
+                if (ta) fm.kget02(koff(La) + (wcode >> (2 * (K - La))), ea0, ea2);
+                if (tb) fm.kget02(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb2);
+                nkm += (uint64_t)ta + (uint64_t)tb;
+                if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
+                if (ta) { oa0 = ea0; oa2 = ea2; }
+                if (tb) { ob0 = eb0; ob2 = eb2; }
+            }
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && !hb) break;
+                const X p0 = h ? pb0 : pa0, o0 = h ? ob0 : oa0;
+                const Z p2 = h ? pb2 : pa2, o2 = h ? ob2 : oa2;
+                const int pe = h ? pbe : pae;
+                const bool keep_hit = c < 0 || o2 < (Z)min_intv;
+                if (keep_hit) {
+                    if (nc == 0 && (S.n1 == 0 || i + 1 < last_start)) {
+                        if (S.n + S.n1 >= S.cap) { ovf = true; return len; }
+                        Intv &m = S.a[S.cap - 1 - S.n1];
+                        m.x[0] = p0; m.x[1] = 0; m.x[2] = p2;
+                        m.info = (uint64_t)(uint32_t)(i + 1) << 32 | (uint32_t)pe;
+                        ++S.n1;
+                        last_start = i + 1;
+                    }
+                } else if (nc == 0 || o2 != last_x2) {
+                    L.set(nc++, o0, o2, pe);
+                    last_x2 = o2;
+                }
+            }
+            j += 2;
+            if (j >= n) {
+                if (nc == 0) phase = 2;
+                else {
+                    n = nc; nc = 0; j = 0; last_x2 = 0;
+                    --i;
+                    c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+                    if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
+                }
+            }
+        }
+        if (phase == 2) break;
+    }
+    return ret;
+}
+
+// smem1_lds (M = false) or smem1_merged (M = true), chosen at compile time per kernel instantiation
+template <bool M, typename X, typename Z, typename Q>
+DEV int smem1_call(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S, bool &ovf,
+                   uint64_t &nblk, uint64_t &nkm)
+{
+    if constexpr (M) return smem1_merged(fm, len, q, x, min_intv, L, S, ovf, nblk, nkm);
+    else return smem1_lds(fm, len, q, x, min_intv, L, S, ovf, nblk, nkm);
+}
+
+template <typename X, typename Z, typename Q>
 DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int max_intv, Intv &mem,
                          uint64_t &nblk, uint64_t &nkm, bool walk)
 {
@@ -617,8 +836,9 @@ __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const 
     for (int i = (int)(threadIdx.x >> 6); i < len; i += 4) d[(size_t)i * 64] = g_codes_stage[s + i];
 }
 
-template <typename X, typename Z, typename Q>
-__global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+// 4 waves per SIMD for u32 rows (16 one-wave blocks per CU, the LDS limit), 3 for 64-bit rows
+template <typename X, typename Z, typename Q, bool M>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
 {
@@ -679,7 +899,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
         int x = 0;
         while (x < len && !ovf) {
             if (q[x] < 4) {
-                x = smem1_lds(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
+                x = smem1_call<M>(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
                 if (!ovf) take_mem1(false);
             } else ++x;
         }
@@ -688,7 +908,7 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
             const Intv p = S.a[k];
             const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
             if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) continue;
-            smem1_lds(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
+            smem1_call<M>(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
             if (!ovf) take_mem1(true);
         }
         if (o.max_mem_intv > 0) {
@@ -738,8 +958,8 @@ __global__ void __launch_bounds__(256) k_smem_lds(DIndex ix, DOpts o, Caps cp, c
 // pass-2 entries that do not qualify skipped, pass changes); a lane that has finished its read sorts its intervals
 // and takes the next read (li += the grid's lanes; lane = li % 64, so the wave-transposed codes and the per-wave
 // slots keep their layouts).  Per read the calls, their order and their arguments are k_smem_lds's: identical intervals.
-template <typename X, typename Z, typename Q>
-__global__ void __launch_bounds__(64) k_smem_lanes(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+template <typename X, typename Z, typename Q, bool M>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lanes(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                    int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                    Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
 {
@@ -815,7 +1035,7 @@ __global__ void __launch_bounds__(64) k_smem_lanes(DIndex ix, DOpts o, Caps cp, 
             }
         }
         if (call_smem) {   // pass 1 and pass 2 share this call site
-            const int r = smem1_lds(fm, len, q, sx, mi, L, S, ovf, nblk, nkm);
+            const int r = smem1_call<M>(fm, len, q, sx, mi, L, S, ovf, nblk, nkm);
             if (!ovf) {   // take_mem1
                 const bool pass2 = st == P2;
                 for (int k = 0; k < S.n1; ++k) {
@@ -899,28 +1119,37 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int L = cp.max_len;
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
-#define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
+    // the merged forward/backward loop of bwt_smem1 (smem1_merged, BSQ_SMEM_MERGE=1; default smem1_lds)
+    const char *me = getenv("BSQ_SMEM_MERGE");
+    const bool merge = me && *me == '1';
+#define BSQ_SMEM_LAUNCH2(X_, Z_, M_)                                                                                   \
     do {                                                                                                               \
         const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
         if (lanes) {                                                                                                   \
             if (codes_t)                                                                                               \
-                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, \
-                                   intv, n_intv, status, ctr, lcap, spill, gcap, L);                                    \
+                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, QT, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t,     \
+                                   offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                          \
             else                                                                                                       \
-                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp,     \
+                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, const uint8_t *, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, \
                                    codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
         } else {                                                                                                       \
             if (codes_t)                                                                                               \
-                hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,   \
-                                   intv, n_intv, status, ctr, lcap, spill, gcap, L);                                    \
+                hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs,  \
+                                   n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                                 \
             else                                                                                                       \
-                hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp,       \
+                hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp,   \
                                    codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
         }                                                                                                              \
+    } while (0)
+#define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
+    do {                                                                                                               \
+        if (merge) BSQ_SMEM_LAUNCH2(X_, Z_, true);                                                                     \
+        else BSQ_SMEM_LAUNCH2(X_, Z_, false);                                                                          \
     } while (0)
     if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t);
     else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
     else BSQ_SMEM_LAUNCH(uint64_t, uint64_t);
+#undef BSQ_SMEM_LAUNCH2
 #undef BSQ_SMEM_LAUNCH
     return hipGetLastError();
 }
