@@ -647,6 +647,19 @@ void orc_profile_get(uint64_t *out) { memcpy(out, orc_prof, sizeof orc_prof); }
 #define PROF(k) ((void)0)
 #endif
 
+/* Seeding trace (tools/seed_model.py: a model of the seeding kernels' schedules): per bwt_smem1 call its forward
+ * and backward trips counted the way smem.hip's kernels take them (the k-mer prefix as one trip, one trip per
+ * extension past it, the unique-interval text walk as one trip per 8 bases; backward: one trip per pair of list
+ * entries per position), per bwt_seed_strategy1 call its trips (one k-mer prefix trip, one per extension past it).
+ * Test infrastructure; off unless orc_seed_trace is used. */
+static __thread int32_t *orc_tr = NULL;
+static __thread int orc_tr_n = 0, orc_tr_cap = 0, orc_tr_pass = 0, orc_tr_k = 0;
+static void tr_push(int kind, int a, int b, int k)
+{
+    if (!orc_tr || orc_tr_n + 4 > orc_tr_cap) return;
+    orc_tr[orc_tr_n++] = kind; orc_tr[orc_tr_n++] = a; orc_tr[orc_tr_n++] = b; orc_tr[orc_tr_n++] = k;
+}
+
 /* bwt_smem1a with max_intv = 0 (as called through bwt_smem1) */
 static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int min_intv, intv_v *mem, intv_v *tmpv)
 {
@@ -660,11 +673,15 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
     prev = &tmpv[0]; curr = &tmpv[1];
     bwt_set_intv(b, q[x], ik);
     ik.info = (uint64_t)(x + 1);
+    int t_pre = 0, t_ext = 0, t_walk = 0, t_bwd = 0;
     for (i = x + 1, curr->n = 0; i < len; ++i) {
         if (ik.x[2] < max_intv) { VPUSH(*curr, ik); break; }
         else if (q[i] < 4) {
             c = 3 - q[i];
             PROF(i - x + 1 <= 11 ? 0 : ik.x[2] == 1 ? 1 : 2);
+            if (i - x + 1 <= 11) t_pre = 1;
+            else if (ik.x[2] == 1 && min_intv <= 1) ++t_walk;
+            else ++t_ext;
             bwt_extend(b, &ik, ok, 0);
             if (ok[c].x[2] != ik.x[2]) {
                 VPUSH(*curr, ik);
@@ -682,6 +699,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
 #ifdef ORC_PROFILE
         if (prev->n == 1 && prev->a[0].x[2] == 1) PROF(9);
 #endif
+        t_bwd += ((int)prev->n + 1) / 2;
         for (j = 0, curr->n = 0; j < (int)prev->n; ++j) {
             bwtintv_t *p = &prev->a[j];
             if (c >= 0 && ik.x[2] >= max_intv) {
@@ -704,6 +722,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
         swap = curr; curr = prev; prev = swap;
     }
     reverse_intvs(mem);
+    tr_push(orc_tr_pass, t_pre + t_ext + (t_walk ? t_walk / 8 + 1 : 0), t_bwd, orc_tr_k);
     return ret;
 }
 
@@ -713,19 +732,25 @@ static int bwt_seed_strategy1(const orc_index *b, int len, const uint8_t *q, int
     memset(mem, 0, sizeof(bwtintv_t));
     if (q[x] > 3) return x + 1;
     bwt_set_intv(b, q[x], ik);
+    int t_pre = 0, t_ext = 0, t_uni = 0;
     for (i = x + 1; i < len; ++i) {
         if (q[i] < 4) {
             c = 3 - q[i];
             PROF(i - x + 1 <= 11 ? 6 : ik.x[2] == 1 ? 7 : 8);
+            if (i - x + 1 <= 11) t_pre = 1;
+            else if (ik.x[2] == 1) ++t_uni;
+            else ++t_ext;
             bwt_extend(b, &ik, ok, 0);
             if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
                 *mem = ok[c];
                 mem->info = (uint64_t)x << 32 | (uint64_t)(i + 1);
+                tr_push(3, t_pre + t_ext, t_uni, orc_tr_k);
                 return i + 1;
             }
             ik = ok[c];
-        } else return i + 1;
+        } else { tr_push(3, t_pre + t_ext, t_uni, orc_tr_k); return i + 1; }
     }
+    tr_push(3, t_pre + t_ext, t_uni, orc_tr_k);
     return len;
 }
 
@@ -1074,9 +1099,11 @@ static void mem_collect_intv(const mopt_t *opt, const orc_index *bwt, int len, c
     int start_width = 1;
     int split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
     mem->n = 0;
+    orc_tr_pass = 1; orc_tr_k = 0;
     while (x < len) {
         if (seq[x] < 4) {
             x = bwt_smem1(bwt, len, seq, x, start_width, mem1, tmpv);
+            ++orc_tr_k;
             for (i = 0; i < (int)mem1->n; ++i) {
                 bwtintv_t *p = &mem1->a[i];
                 int slen = (int)((uint32_t)p->info - (p->info >> 32));
@@ -1085,10 +1112,12 @@ static void mem_collect_intv(const mopt_t *opt, const orc_index *bwt, int len, c
         } else ++x;
     }
     old_n = (int)mem->n;
+    orc_tr_pass = 2;
     for (k = 0; k < old_n; ++k) {
         bwtintv_t p = mem->a[k];
         int start = (int)(p.info >> 32), end = (int32_t)p.info;
         if (end - start < split_len || p.x[2] > (uint64_t)opt->split_width) continue;
+        orc_tr_k = k;
         bwt_smem1(bwt, len, seq, (start + end) >> 1, (int)p.x[2] + 1, mem1, tmpv);
         for (i = 0; i < (int)mem1->n; ++i)
             if ((uint32_t)mem1->a[i].info - (mem1->a[i].info >> 32) >= (uint64_t)opt->min_seed_len)
@@ -1096,10 +1125,12 @@ static void mem_collect_intv(const mopt_t *opt, const orc_index *bwt, int len, c
     }
     if (opt->max_mem_intv > 0) {
         x = 0;
+        orc_tr_k = 0;
         while (x < len) {
             if (seq[x] < 4) {
                 bwtintv_t m;
                 x = bwt_seed_strategy1(bwt, len, seq, x, opt->min_seed_len, opt->max_mem_intv, &m);
+                ++orc_tr_k;
                 if (m.x[2] > 0) VPUSH(*mem, m);
             } else ++x;
         }
@@ -1850,6 +1881,19 @@ static mem_aln_t mem_reg2aln(const mopt_t *opt, const orc_index *bns, int l_quer
 /* ============================================================================================== */
 /* public entry points                                                                             */
 /* ============================================================================================== */
+/* The seeding trace of one read (see tr_push): 4 int32 per call {kind (1 pass-1 smem, 2 pass-2 smem, 3 seed strategy),
+ * forward trips (or SS trips before its interval is unique), backward trips (or SS steps on a unique interval), call index (pass 1 / SS: ordinal; pass 2:
+ * the mem index k)}; returns the number of int32 written (at most cap). */
+int orc_seed_trace(const orc_index *idx, const orc_opts *o, const uint8_t *q, int len, int32_t *out, int cap)
+{
+    orc_tr = out; orc_tr_n = 0; orc_tr_cap = cap;
+    uint64_t tmp[4 * 512];
+    orc_collect_intv(idx, o, q, len, tmp, 512);
+    const int n = orc_tr_n;
+    orc_tr = NULL; orc_tr_n = 0; orc_tr_cap = 0;
+    return n;
+}
+
 int orc_collect_intv(const orc_index *idx, const orc_opts *o, const uint8_t *q, int len, uint64_t *out, int max)
 {
     mopt_t opt; make_opt(o, &opt);
