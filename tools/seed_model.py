@@ -107,6 +107,11 @@ def main():
         for w in range(waves * rpl):
             tot += wave_lds(tr[w * 64:(w + 1) * 64], name == "merged")
         res[name] = tot
+    # tools/exp_sort_seed.py's measured orderings (C2 lds: 10.57 ms as generated, 9.31 ms sorted descending by
+    # interval count): the same schedule over reads sorted by their number of calls and by their trips
+    for name, key in (("lds_bycalls", lambda c: -len(c)), ("lds_bytrips", lambda c: -sum(x[1] + x[2] for x in c))):
+        st = sorted(tr, key=key)
+        res[name] = sum(wave_lds(st[w * 64:(w + 1) * 64], False) for w in range(waves * rpl))
     for name in ("lanes", "lanesm"):
         tot = 0
         for w in range(waves):
