@@ -673,7 +673,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
     prev = &tmpv[0]; curr = &tmpv[1];
     bwt_set_intv(b, q[x], ik);
     ik.info = (uint64_t)(x + 1);
-    int t_pre = 0, t_ext = 0, t_walk = 0, t_bwd = 0;
+    int t_pre = 0, t_ext = 0, t_walk = 0, t_bwd = 0, t_pos = 0, t_pos12 = 0, t_pos1u = 0;
     for (i = x + 1, curr->n = 0; i < len; ++i) {
         if (ik.x[2] < max_intv) { VPUSH(*curr, ik); break; }
         else if (q[i] < 4) {
@@ -700,6 +700,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
         if (prev->n == 1 && prev->a[0].x[2] == 1) PROF(9);
 #endif
         t_bwd += ((int)prev->n + 1) / 2;
+        ++t_pos; t_pos12 += prev->n <= 2; t_pos1u += prev->n == 1 && prev->a[0].x[2] == 1;
         for (j = 0, curr->n = 0; j < (int)prev->n; ++j) {
             bwtintv_t *p = &prev->a[j];
             if (c >= 0 && ik.x[2] >= max_intv) {
@@ -723,6 +724,7 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
     }
     reverse_intvs(mem);
     tr_push(orc_tr_pass, t_pre + t_ext + (t_walk ? t_walk / 8 + 1 : 0), t_bwd, orc_tr_k);
+    tr_push(4, t_pos, t_pos12, t_pos1u);
     return ret;
 }
 

@@ -26,6 +26,9 @@ from bioseqdb_amd import BwaIndex, NucleotideSequence, synth  # noqa: E402
 from bioseqdb_amd._native import lib  # noqa: E402
 
 
+BWD_POS = [0, 0, 0]
+
+
 def traces(n_reads, ref_bp=100_000_000, walk=True):
     ref = synth.make_reference(ref_bp)
     pi, oi = BwaIndex(), O.OracleIndex()
@@ -51,6 +54,10 @@ def traces(n_reads, ref_bp=100_000_000, walk=True):
         calls = []
         for k in range(0, m, 4):
             kind, a, b, idx = buf[k], buf[k + 1], buf[k + 2], buf[k + 3]
+            if kind == 4:   # backward positions of the preceding smem call: all, with <= 2 entries, one unique entry
+                for j, v in enumerate((a, b, idx)):
+                    BWD_POS[j] += v
+                continue
             if kind == 3:   # seed strategy: trips before uniqueness, then the walk (2 trips) or one per step
                 calls.append((3, a + (min(b, 2) if walk else b), 0, idx))
             else:
@@ -123,6 +130,8 @@ def main():
         ideal += max(sum(sum(c[1] + c[2] for c in tr[(w * 64 + l) + 64 * waves * k]) for k in range(rpl)) for l in range(64))
     res["ideal"] = ideal
     print(f"{n} reads, {waves} waves x {rpl} reads per lane; lane work {work / n:.1f} trips per read")
+    print(f"  backward positions per read {BWD_POS[0] / n:.1f}: {BWD_POS[1] / max(BWD_POS[0], 1):.3f} with <= 2 list "
+          f"entries, {BWD_POS[2] / max(BWD_POS[0], 1):.3f} with one unique entry")
     for k, v in res.items():
         print(f"  {k:7s} wave trips per 64 reads {v * 64 / n:8.1f}   useful lane-trips {work / (v * 64):.3f}")
 
