@@ -620,7 +620,7 @@ def main() -> int:
                          "batch runs over the K steps")
     ap.add_argument("--cursor-only", action="store_true",
                     help="after the timed steps, only the pipelined cursor measurement (profiling the drop-in loop)")
-    ap.add_argument("--cursor-depth", type=int, default=8,
+    ap.add_argument("--cursor-depth", type=int, default=16,
                     help="fetches in flight in the sql_cursor measurement (BwaIndex::pipeline_depth's default)")
     ap.add_argument("--seed-offset", type=int, default=0,
                     help="rank (or member) k aligns the reads of seed READ_SEED + k + offset, lrand48 position "
@@ -1045,7 +1045,7 @@ def main() -> int:
             N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
 
         # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
-        # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (8) (each fetch staged, then its tuples released),
+        # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (16) (each fetch staged, then its tuples released),
         # the oldest fetch's rows taken when the pipeline is full; with the two nuclseq columns per row
         # (build_tuple_bwa) rendered on the GPU, and without them
         hb.phase = "pipelined cursor fetches"

@@ -84,7 +84,7 @@ struct bsq_pipeline {
     std::vector<std::unique_ptr<Slot>> s;
     uint64_t n_submit = 0, n_take = 0, n_release = 0;   // slot of job j is s[j % S]
     uint64_t run_started = 0;                           // jobs whose alignment turn has begun
-    int running = 0, run_cap = 4;                       // alignments on the device now, and at most
+    int running = 0, run_cap = 6;                       // alignments on the device now, and at most
     int route_via = -1;                                 // record route of the slots' batches (group exchange)
     std::vector<std::array<double, 7>> trace;           // BSQ_PIPE_TRACE: per job, slot then Slot::t
     std::mutex mu;
@@ -350,10 +350,11 @@ extern "C" int bsq_pipeline_create(bsq_index *idx, int n_slots, bsq_pipeline **o
     std::unique_ptr<bsq_pipeline> p(new (std::nothrow) bsq_pipeline());
     if (!p) return fail(BSQ_E_NOMEM, "out of memory");
     p->idx = idx;
-    {   // concurrent alignments: 4 measure best on one MI355X (3-6 within 1 %, 8 lose 20 %)
+    {   // concurrent alignments: 6 measure best on one MI355X with 16 fetches in flight and 8 HIP hardware queues
+        // (4 at depth 8 41 M reads/s, 6-7 at depth 16 44-46 M; 16 or 24 queues 25-38 M)
         const char *e = getenv("BSQ_PIPE_RUN");
-        const int v = e ? atoi(e) : 4;
-        p->run_cap = std::max(1, std::min(v > 0 ? v : 4, 64));
+        const int v = e ? atoi(e) : 6;
+        p->run_cap = std::max(1, std::min(v > 0 ? v : 6, 64));
     }
     for (int k = 0; k < n_slots; ++k) p->s.emplace_back(new Slot());
     for (auto &x : p->s) x->th = std::thread(worker, p.get(), x.get());

@@ -100,10 +100,10 @@ int BwaIndex::pipeline_depth() const
 {
     if (devices_.size() > 1) return 1;   // a group aligns its fetch at submit (every member pipelines its shard)
     const char *e = getenv("BSQ_PIPE_DEPTH");
-    // 8 fetches in flight: up to 4 align at once (bsq_pipeline's run cap) while the next ones are staged and
-    // uploaded, so a new alignment starts as soon as one ends (bench.py sql_cursor)
-    const int d = e ? atoi(e) : 8;
-    return std::max(1, std::min(d, 16));
+    // 16 fetches in flight: up to 6 align at once (bsq_pipeline's run cap) while the next ones are staged and
+    // uploaded, so a new alignment starts as soon as one ends (bench.py sql_cursor; DESIGN.md §3b round 5)
+    const int d = e ? atoi(e) : 16;
+    return std::max(1, std::min(d, 32));
 }
 
 void BwaIndex::ensure_pipe() const
