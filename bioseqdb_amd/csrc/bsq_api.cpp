@@ -1189,11 +1189,18 @@ int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
         max_len = std::max(max_len, part[(size_t)t].max_len);
     }
     const int64_t bytes = base_in[(size_t)T];
-    if (bytes > s.host_cap) {
+    // the pinned buffer also holds copies of meta and offs after the varlenas: the upload copies all three from
+    // pinned memory (pageable sources go through the HIP runtime's staging buffer, one copy at a time per process,
+    // which serialised the uploads of concurrent pipeline slots: DESIGN.md §3b round 5)
+    size_t n_holed = 0;
+    for (const Part &q : part) n_holed += q.holed.size();
+    const int64_t meta_at = (bytes + 15) & ~15ll, offs_at = meta_at + 8 * (int64_t)(2 * (n + 1) + n_holed);
+    const int64_t need = offs_at + 8 * (int64_t)(n + 1);
+    if (need > s.host_cap) {
         if (s.host) hipHostFree(s.host);
         s.host = nullptr;
         s.host_cap = 0;
-        const int64_t cap = std::max<int64_t>(bytes + bytes / 4, 4096);
+        const int64_t cap = std::max<int64_t>(need + need / 4, 4096);
         if (hipHostMalloc((void **)&s.host, (size_t)cap) != hipSuccess) { s.host = nullptr; set_err("out of pinned host memory"); return BSQ_E_NOMEM; }
         s.host_cap = cap;
     }
@@ -1212,6 +1219,18 @@ int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
     poff[n] = base_pac[(size_t)T];
     boff[n] = base_b[(size_t)T];
     for (const Part &q : part) s.meta.insert(s.meta.end(), q.holed.begin(), q.holed.end());
+    {   // pinned copies of meta and offs (by range on the staging threads)
+        int64_t *pm = reinterpret_cast<int64_t *>(s.host + meta_at), *po = reinterpret_cast<int64_t *>(s.host + offs_at);
+        const size_t nm = s.meta.size(), no = n + 1;
+        run([&](int t) {
+            const size_t a = nm * (size_t)t / (size_t)T, b = nm * (size_t)(t + 1) / (size_t)T;
+            memcpy(pm + a, s.meta.data() + a, (b - a) * 8);
+            const size_t c = no * (size_t)t / (size_t)T, d = no * (size_t)(t + 1) / (size_t)T;
+            memcpy(po + c, s.offs.data() + c, (d - c) * 8);
+        });
+    }
+    s.meta_at = meta_at;
+    s.offs_at = offs_at;
     s.n = n_reads;
     s.max_len = max_len;
     s.bases = boff[n];
@@ -1233,8 +1252,8 @@ int batch_upload_staged(bsq_batch *b, const NsStage &s)
     if (n) {
         hipStream_t st = b->stream;
         HIPCHK(hipMemcpyAsync(b->ns_dev, s.host, (size_t)s.host_bytes, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(b->ns_meta, s.meta.data(), s.meta.size() * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(b->offs, s.offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->ns_meta, s.host + s.meta_at, s.meta.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(b->offs, s.host + s.offs_at, (n + 1) * 8, hipMemcpyHostToDevice, st));
         const DecView v{b->ns_dev, b->ns_meta, b->ns_meta + n + 1, b->offs, (int64_t)n, s.meta[2 * n + 1]};
         HIPCHK(launch_dec_codes(st, v, b->ns_meta + 2 * (n + 1), (int64_t)(s.meta.size() - 2 * (n + 1)), b->codes));
     }

@@ -22,6 +22,7 @@ struct NsStage {
     std::vector<int64_t> offs;    // base offsets [n+1]
     uint8_t *host = nullptr;      // packed varlenas (pinned)
     int64_t host_cap = 0, host_bytes = 0;
+    int64_t meta_at = 0, offs_at = 0;   // pinned copies of meta and offs at host + meta_at / host + offs_at
     NsStage() = default;
     NsStage(const NsStage &) = delete;
     NsStage &operator=(const NsStage &) = delete;
