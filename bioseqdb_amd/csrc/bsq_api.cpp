@@ -1102,15 +1102,16 @@ static int prepare_workspace(bsq_batch *b, int max_len)
 {
     const int32_t want = max_len > 150 ? std::max<int32_t>(1, std::min<int64_t>(b->chunk0, (int64_t)b->chunk0 * 150 / max_len))
                                        : b->chunk0;
-    if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1) || want != b->chunk) {
+    // (a workspace lent by a pipeline's pool may hold more reads than this batch's pass: it is used as it is)
+    if (!b->main.status || b->main.cp.max_len < max_len || tiny_caps() != (b->main.cp.regs == 1) || b->main.max_reads < want) {
         b->main.release();
-        b->chunk = want;
         // per-thread scratch: the main pass's reg2aln keeps its traceback in LDS and the zslab unless reads are
         // longer than 1024 bases (then the serial kernel's 32 KB traceback area is needed)
-        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), b->chunk, device_workers(b->device),
+        int rc = ws_alloc(b->main, main_caps(std::max(max_len, 1)), want, device_workers(b->device),
                           max_len > 1024 ? 32 * 1024 : 0, false);
         if (rc) return rc;
     }
+    b->chunk = want;
     return BSQ_OK;
 }
 
@@ -1138,7 +1139,8 @@ int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
     s.host_bytes = 0;
     const size_t n = (size_t)n_reads;
     // Two passes over contiguous ranges of the reads, on up to 8 host threads for a large fetch (a cursor
-    // fetch of 256k reads is ~13 MB of varlenas): sizes and offsets, then the copy into pinned memory.
+    // fetch of 256k reads is ~13 MB of varlenas): sizes and offsets, then the copy into pinned memory.  A pipeline
+    // stages its deferred fetches one at a time in submission order (pipeline.cpp prep_job).
     const int T = n >= 65536 ? (int)std::max<unsigned>(1, std::min<unsigned>(8, std::thread::hardware_concurrency())) : 1;
     std::vector<size_t> lo((size_t)T + 1);
     for (int t = 0; t <= T; ++t) lo[(size_t)t] = n * (size_t)t / (size_t)T;
@@ -1238,7 +1240,7 @@ int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n_reads)
     return BSQ_OK;
 }
 
-int batch_upload_staged(bsq_batch *b, const NsStage &s)
+int batch_upload_staged(bsq_batch *b, const NsStage &s, bool with_workspace)
 {
     if (s.n > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
     if (s.bases > b->max_bases) { set_err("batch holds at most %lld bases", (long long)b->max_bases); return BSQ_E_INVALID; }
@@ -1249,17 +1251,62 @@ int batch_upload_staged(bsq_batch *b, const NsStage &s)
     b->h_offs = s.offs;
     b->n_reads = s.n;
     b->max_len = s.max_len;
+    hipStream_t st = b->stream;
     if (n) {
-        hipStream_t st = b->stream;
         HIPCHK(hipMemcpyAsync(b->ns_dev, s.host, (size_t)s.host_bytes, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(b->ns_meta, s.host + s.meta_at, s.meta.size() * 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(b->offs, s.host + s.offs_at, (n + 1) * 8, hipMemcpyHostToDevice, st));
         const DecView v{b->ns_dev, b->ns_meta, b->ns_meta + n + 1, b->offs, (int64_t)n, s.meta[2 * n + 1]};
         HIPCHK(launch_dec_codes(st, v, b->ns_meta + 2 * (n + 1), (int64_t)(s.meta.size() - 2 * (n + 1)), b->codes));
     }
-    { const int rc = prepare_workspace(b, s.max_len); if (rc) return rc; }
-    HIPCHK(hipStreamSynchronize(b->stream));   // the staged buffers may be reused when this returns
+    if (with_workspace) { const int rc = prepare_workspace(b, s.max_len); if (rc) return rc; }
+    HIPCHK(hipStreamSynchronize(st));   // the staged buffers may be reused when this returns
     return BSQ_OK;
+}
+
+// A batch's workspaces (the main pass's and the retry levels') as a unit a pipeline lends to the batch whose
+// alignment turn it is: up to run_cap alignments run at once, so a pipeline of 16 fetches needs run_cap sets of
+// ~8.5 GB (262,144-read passes), not 16 (pipeline.cpp).
+struct WsSet {
+    Workspace main, retry[N_RETRY_LEVELS];
+};
+
+WsSet *batch_detach_workspaces(bsq_batch *b)
+{
+    hipSetDevice(b->device);
+    hipStreamSynchronize(b->stream);   // nothing on the batch's stream may still use them
+    WsSet *w = new (std::nothrow) WsSet();
+    if (!w) return nullptr;
+    std::swap(w->main, b->main);
+    for (int i = 0; i < N_RETRY_LEVELS; ++i) std::swap(w->retry[i], b->retry[i]);
+    return w;
+}
+
+bool batch_has_workspace(const bsq_batch *b) { return b->main.status != nullptr; }
+
+void batch_attach_workspaces(bsq_batch *b, WsSet *w)
+{
+    if (!w) return;
+    hipSetDevice(b->device);
+    b->main.release();
+    for (auto &r : b->retry) r.release();
+    std::swap(w->main, b->main);
+    for (int i = 0; i < N_RETRY_LEVELS; ++i) std::swap(w->retry[i], b->retry[i]);
+    delete w;
+}
+
+void workspaces_free(WsSet *w)
+{
+    if (!w) return;
+    w->main.release();
+    for (auto &r : w->retry) r.release();
+    delete w;
+}
+
+int batch_prepare_workspace(bsq_batch *b)
+{
+    HIPCHK(hipSetDevice(b->device));
+    return prepare_workspace(b, std::max(b->max_len, 1));
 }
 
 }  // namespace bsq
@@ -1269,7 +1316,7 @@ extern "C" int bsq_batch_set_nuclseqs(bsq_batch *b, const void *const *reads, in
     if (!b || n_reads < 0 || (n_reads && !reads)) { set_err("invalid argument"); return BSQ_E_INVALID; }
     if (n_reads > b->max_reads) { set_err("batch holds at most %d reads", b->max_reads); return BSQ_E_INVALID; }
     { const int rc = stage_nuclseqs(b->stage, reads, n_reads); if (rc) return rc; }
-    return batch_upload_staged(b, b->stage);
+    return batch_upload_staged(b, b->stage, true);
 }
 
 static int env_int(const char *name, int dflt)
@@ -1693,6 +1740,9 @@ extern "C" int bsq_batch_run(bsq_batch *b, const bsq_opts *opts, uint64_t first_
     const int n = b->n_reads;
     const DOpts o = make_dopts(*opts);
     hipStream_t st = b->stream;
+    // a batch whose workspaces a pipeline took back (pipeline.cpp: a group's held shares re-run by
+    // bsq_batch_run_rounds) gets its own again; a no-op when they fit
+    if (n > 0) { const int rc = prepare_workspace(b, std::max(b->max_len, 1)); if (rc) return rc; }
     // lrand48 ids: read i consumes call first_call_seq + i (computed on the device)
     if (n) hipLaunchKernelGGL(k_lrand_ids, dim3((n + 255) / 256), dim3(256), 0, st, (uint64_t)first_call_seq, n, b->ids);
     HIPCHK(hipGetLastError());
@@ -1870,6 +1920,8 @@ extern "C" int bsq_batch_seed(bsq_batch *b, const bsq_opts *opts)
     b->seed_off.clear();
     b->seed_intv.clear();
     b->retried = 0;
+    // a batch whose workspaces a pipeline took back (pipeline.cpp) gets its own again
+    if (n > 0) { const int rc = prepare_workspace(b, std::max(b->max_len, 1)); if (rc) return rc; }
     HIPCHK(hipMemsetAsync(b->ctr, 0, sizeof(Counters) * STG_N, b->stream));
     for (int s = 0; s < STG_N; ++s) { b->stage_ms[s] = 0; b->stage_bytes[s] = 0; b->stage_work[s] = 0; }
     if (n > 0 && b->idx->h.seq_len > 0) {

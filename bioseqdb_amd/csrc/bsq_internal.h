@@ -31,8 +31,18 @@ struct NsStage {
 
 // Validates and packs n reads (errors: BSQ_E_INVALID / BSQ_E_NOMEM with the thread's message set).
 int stage_nuclseqs(NsStage &s, const void *const *reads, int32_t n);
-// H2D of a staged fetch into batch b, nt4 conversion on the device, workspace sizing; synchronous.
-int batch_upload_staged(bsq_batch *b, const NsStage &s);
+// H2D of a staged fetch into batch b, nt4 conversion on the device, and (with_workspace) workspace sizing;
+// synchronous.
+int batch_upload_staged(bsq_batch *b, const NsStage &s, bool with_workspace);
+// A batch's device workspaces as a unit (pipeline.cpp lends run_cap sets to the batches whose alignment turn it is):
+// detach (after syncing the batch's stream; an empty set when the batch holds none), attach (frees what the batch
+// held), free; batch_prepare_workspace sizes the attached set for the uploaded reads.
+struct WsSet;
+WsSet *batch_detach_workspaces(bsq_batch *b);
+void batch_attach_workspaces(bsq_batch *b, WsSet *w);
+bool batch_has_workspace(const bsq_batch *b);
+void workspaces_free(WsSet *w);
+int batch_prepare_workspace(bsq_batch *b);
 int32_t batch_max_reads(const bsq_batch *b);
 int64_t batch_max_bases(const bsq_batch *b);
 

@@ -84,9 +84,11 @@ struct bsq_pipeline {
     std::vector<std::unique_ptr<Slot>> s;
     uint64_t n_submit = 0, n_take = 0, n_release = 0;   // slot of job j is s[j % S]
     uint64_t run_started = 0;                           // jobs whose alignment turn has begun
+    uint64_t stage_turn = 0;                            // the job whose staging may run (submission order)
     int running = 0, run_cap = 6;                       // alignments on the device now, and at most
     int route_via = -1;                                 // record route of the slots' batches (group exchange)
     std::vector<std::array<double, 7>> trace;           // BSQ_PIPE_TRACE: per job, slot then Slot::t
+    std::vector<WsSet *> pool;                          // device workspaces between alignment turns (<= run_cap)
     std::mutex mu;
     std::condition_variable cv;
     bool stop = false;
@@ -104,6 +106,25 @@ void drop_cols(Slot &x)
 int prep_job(bsq_pipeline *p, Slot &x)
 {
     x.t[1] = now_ms();
+    // Staging turns go in submission order: a deferred fetch is staged on all of stage_nuclseqs' threads while the
+    // fetches behind it wait, so the first fetches reach the device first (16 stagings at once put ~128 threads on
+    // the caller's cores and delayed every one of them).  Every job takes its turn, staged or not.
+    {
+        std::unique_lock<std::mutex> lk(p->mu);
+        p->cv.wait(lk, [&] { return x.job == p->stage_turn; });
+    }
+    struct Turn {   // passes the staging turn on exactly once (early returns included)
+        bsq_pipeline *p;
+        void pass()
+        {
+            if (!p) return;
+            std::lock_guard<std::mutex> lk(p->mu);
+            ++p->stage_turn;
+            p->cv.notify_all();
+            p = nullptr;
+        }
+        ~Turn() { pass(); }
+    } turn{p};
     if (const char *e = getenv("BSQ_PIPE_FAILPOINT")) {   // tests: job number e fails here (a failed fetch)
         if (*e && strtoull(e, nullptr, 10) == x.job) {
             std::lock_guard<std::mutex> lk(p->mu);
@@ -127,6 +148,7 @@ int prep_job(bsq_pipeline *p, Slot &x)
     } else if (x.mode == PipeMode::COPY) {
         x.resident = false;
     }
+    turn.pass();   // the upload below runs beside the next job's staging
     if (x.n == 0 || bsq_index_seq_len(p->idx) <= 0) return BSQ_OK;
     if (!x.batch || x.cap_reads < x.stage.n || x.cap_bases < x.stage.bases) {
         bsq_batch_free(x.batch);
@@ -142,7 +164,7 @@ int prep_job(bsq_pipeline *p, Slot &x)
     }
     { const int rc = bsq_batch_set_record_route(x.batch, p->route_via); if (rc) return rc; }   // no-op when unchanged
     if (!x.resident) {
-        const int rc = batch_upload_staged(x.batch, x.stage);
+        const int rc = batch_upload_staged(x.batch, x.stage, false);   // workspaces come with the alignment turn
         if (rc) return rc;
         x.resident = true;
     }
@@ -161,7 +183,25 @@ int align_job(bsq_pipeline *p, Slot &x)
         x.view = &x.empty;
         return BSQ_OK;
     }
-    { const int rc = bsq_batch_run(x.batch, &x.opts, x.first_call); if (rc) return rc; }
+    // The device workspaces (~8.5 GB per 262,144-read pass) are lent for the turn: at most run_cap alignments run
+    // at once, so the pipeline holds run_cap sets however many fetches wait staged and uploaded (16 sets of 16
+    // slots did not fit beside a 3 Gbp index).  Sets of the same shape are reused as they are.
+    // (A batch that ran outside the pipeline since -- a group's held shares -- may hold its own set: it keeps it.)
+    WsSet *ws = nullptr;
+    if (!batch_has_workspace(x.batch)) {
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (!p->pool.empty()) { ws = p->pool.back(); p->pool.pop_back(); }
+    }
+    batch_attach_workspaces(x.batch, ws);
+    int rc = batch_prepare_workspace(x.batch);
+    if (!rc) rc = bsq_batch_run(x.batch, &x.opts, x.first_call);
+    const std::string err = rc ? std::string(bsq_last_error()) : std::string();
+    ws = batch_detach_workspaces(x.batch);
+    if (ws) {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->pool.push_back(ws);
+    }
+    if (rc) { set_error(err); return rc; }
     x.t[3] = now_ms();
     x.view = bsq_batch_hits(x.batch);
     return BSQ_OK;
@@ -305,6 +345,7 @@ int pipeline_rewind(bsq_pipeline *p)
     if (p->n_release != p->n_submit) return fail(BSQ_E_INVALID, "pipeline has outstanding submissions");
     p->n_submit = p->n_take = p->n_release = 0;
     p->run_started = 0;
+    p->stage_turn = 0;
     return BSQ_OK;
 }
 
@@ -387,6 +428,7 @@ extern "C" void bsq_pipeline_free(bsq_pipeline *p)
         drop_cols(*x);
         bsq_batch_free(x->batch);
     }
+    for (WsSet *w : p->pool) workspaces_free(w);
     delete p;
 }
 
