@@ -331,7 +331,9 @@ static int kmer_depth(uint64_t seq_len)
     if (seq_len == 0) return 0;
     int K = 0;
     while (K < 11 && (1ull << (2 * (K + 1))) <= seq_len) ++K;   // ~log4(rows), at most 11
-    if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(11, atoi(e)));   // the kernels' preload cap
+    // BSQ_KMER_K: 0 disables; up to 15 (the kernels preload levels <= 11 and read deeper levels one per step;
+    // 32-bit table indices and codes)
+    if (const char *e = getenv("BSQ_KMER_K")) K = std::max(0, std::min(15, atoi(e)));
     return K;
 }
 

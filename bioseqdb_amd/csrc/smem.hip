@@ -329,8 +329,9 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
         // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
         // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
         // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
-        constexpr int KM = 11;   // kmer_depth() never exceeds 11
-        const int Lt = fm.K < len - x ? fm.K : len - x;
+        constexpr int KM = 11;   // rows preloaded; a deeper table (kmer_depth up to 15) serves lengths KM+1..K below
+        const int Kp = fm.K < KM ? fm.K : KM;
+        const int Lt = Kp < len - x ? Kp : len - x;
         int cb[KM + 1];
 #pragma unroll
         for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
@@ -533,8 +534,9 @@ DEV int smem1_merged(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X
         // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
         // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
         // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
-        constexpr int KM = 11;   // kmer_depth() never exceeds 11
-        const int Lt = fm.K < len - x ? fm.K : len - x;
+        constexpr int KM = 11;   // rows preloaded; a deeper table (kmer_depth up to 15) serves lengths KM+1..K below
+        const int Kp = fm.K < KM ? fm.K : KM;
+        const int Lt = Kp < len - x ? Kp : len - x;
         int cb[KM + 1];
 #pragma unroll
         for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
@@ -1273,7 +1275,7 @@ __global__ void __launch_bounds__(64) k_smem_sm(DIndex ix, DOpts o, Caps cp, con
     fm.l2_3 = (uint32_t)ix.L2[3]; fm.l2_4 = (uint32_t)ix.L2[4];
     fm.primary = (uint32_t)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
-    fm.K = ix.kmer_k;
+    fm.K = ix.kmer_k < 11 ? ix.kmer_k : 11;   // this kernel uses levels <= 11 of a deeper table
     fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
     const int K = fm.K;
     // LDS (u32 units): the read's nwp words lane-interleaved, then the list [x0: 64*lcap][x2: 64*lcap][end: 64*lcap u16]

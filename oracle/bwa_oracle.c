@@ -640,7 +640,7 @@ static void reverse_intvs(intv_v *p)
 #ifdef ORC_PROFILE
 /* seeding work profile (tools/seed_profile.py): bwt_extend calls by phase and by what the interval is
  * (the string fits the GPU k-mer table / the interval has one occurrence / other) */
-uint64_t orc_prof[12];
+uint64_t orc_prof[16];   /* [12..15]: backward extensions of strings of 12..15 bases */
 void orc_profile_get(uint64_t *out) { memcpy(out, orc_prof, sizeof orc_prof); }
 #define PROF(k) (++orc_prof[k])
 #else
@@ -705,6 +705,9 @@ static int bwt_smem1(const orc_index *b, int len, const uint8_t *q, int x, int m
             bwtintv_t *p = &prev->a[j];
             if (c >= 0 && ik.x[2] >= max_intv) {
                 PROF((int)(uint32_t)p->info - i <= 11 ? 3 : p->x[2] == 1 ? 4 : 5);
+#ifdef ORC_PROFILE
+                { const int sl = (int)(uint32_t)p->info - i; if (sl >= 12 && sl <= 15) PROF(sl); }
+#endif
                 bwt_extend(b, p, ok, 1);
             }
             if (c < 0 || ik.x[2] < max_intv || ok[c].x[2] < (uint64_t)min_intv) {

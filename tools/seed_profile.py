@@ -39,10 +39,13 @@ opts = O.opts_from(type("o", (), dict(min_seed_len=19, max_occ=500, a=1, b=4, pe
 codes = np.ascontiguousarray(reads.codes); offs = np.ascontiguousarray(reads.offsets)
 ck = ctypes.c_uint64()
 P.orc_seed_batch(oi.h, ctypes.byref(opts), codes.ctypes.data, offs.ctypes.data, reads.n, 1, ctypes.byref(ck))
-c = (ctypes.c_uint64 * 12)()
+c = (ctypes.c_uint64 * 16)()
 P.orc_profile_get(c)
 names = ["fwd<=11", "fwd u1", "fwd rank", "bwd<=11", "bwd u1", "bwd rank", "strat<=11", "strat u1", "strat rank",
-         "bwd levels with a lone unique entry"]
+         "bwd levels with a lone unique entry", "", "",
+         "bwd rank, string of 12 bases", "bwd rank, 13 bases", "bwd rank, 14 bases", "bwd rank, 15 bases"]
 tot = sum(c[:9])
 for k, nm in enumerate(names):
+    if not nm:
+        continue
     print(f"{nm:38s} {c[k] / reads.n:8.1f} per read" + (f"  {100 * c[k] / tot:5.1f}%" if k < 9 else ""))
