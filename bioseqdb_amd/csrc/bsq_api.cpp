@@ -329,11 +329,12 @@ struct IndexMeta {   // fixed header of the metadata blob; followed by Ann[n_ann
 static int kmer_depth(uint64_t seq_len)
 {
     if (seq_len == 0) return 0;
-    // ~log4(rows), at most 11 while the rank blocks (32 B per 64 rows) fit the 256 MB Infinity Cache beside the
-    // table (C3: 100 MB + 89 MB; a deeper table's lines miss it and lose to the cached rank blocks they replace),
-    // else at most 13: the rank blocks' lines miss anyway and each level answers more backward extensions with one
-    // line (C4, 3 Gbp: 28.0 M reads/s at 11, 30.0 M at 13 with a 2.9 GB table)
-    const int kmax = seq_len / 2 > (256ull << 20) ? 13 : 11;
+    // ~log4(rows), at most 10 while the rank blocks (32 B per 64 rows) fit the 256 MB Infinity Cache: the table
+    // competes with them for it (C3, 100 MB of rank blocks: seeding 10.45 ms at K = 10 with a 22 MB table, 10.7 at
+    // 11 with 89 MB, 11.3-12.1 at 12-14, 10.9 at 9); else at most 13: the rank blocks' lines miss anyway and each
+    // level answers more backward extensions with one line (C4, 3 Gbp: 28.0 M reads/s at 11, 30.0 M at 13 with a
+    // 2.9 GB table)
+    const int kmax = seq_len / 2 > (256ull << 20) ? 13 : 10;
     int K = 0;
     while (K < kmax && (1ull << (2 * (K + 1))) <= seq_len) ++K;
     // BSQ_KMER_K: 0 disables; up to 15 (the kernels preload levels <= 11 and read deeper levels one per step;

@@ -140,6 +140,23 @@ def test_parity_wide_rows(monkeypatch, force, lcap):
     assert not bad, bad[:20]
 
 
+@pytest.mark.parametrize("force,k", [("0", "13"), ("1", "13"), ("2", "13"), ("0", "0")],
+                         ids=["u32_k13", "z32_k13", "z64_k13", "no_table"])
+def test_parity_kmer_table_depth(monkeypatch, force, k):
+    """k-mer tables deeper than the 11 levels the seeding kernels preload (levels past 11 read one per step in the
+    forward loop, the seed strategy and the backward phase; the C4 default is 13) and no table at all give the
+    oracle's rows.  BSQ_KMER_K forces the depth on a small reference (the default here is 10)."""
+    monkeypatch.setenv("BSQ_KMER_K", k)
+    if force != "0":
+        monkeypatch.setenv("BSQ_FORCE_WIDE", force)
+    ref = synth.make_reference(1_000_000, n_rows=3, n_run_every=300_000, n_run_len=400, dup_frac=0.02)
+    reads = synth.make_reads(ref, 3000, seed=43)
+    pi, oi = build_pair([t.decode() for t in ref.texts()])
+    rows, bad = compare(pi, oi, _texts(reads), first_call=11)
+    assert rows > 2500
+    assert not bad, bad[:20]
+
+
 def test_parity_chunked_batch(monkeypatch):
     """A batch larger than the workspace runs in chunks (reads resident, workspace reused); the
     retry pass and the read/CIGAR offsets are per chunk, the results must be unchanged."""
