@@ -934,6 +934,12 @@ struct EhG {
     bool *ovf = nullptr;
     DEV int2 get(int j) const { return p[j]; }
     DEV void set(int j, int2 v) const { p[j] = v; }
+    // the cell loop's cursor over consecutive columns (EhRing keeps an LDS byte address instead)
+    using Cur = int;
+    DEV Cur cur(int j) const { return j; }
+    DEV Cur adv(Cur c) const { return c + 1; }
+    DEV int2 at(Cur c) const { return get(c); }
+    DEV void put(Cur c, int2 v) const { set(c, v); }
 };
 extern __shared__ uint32_t g_lds_eh[];   // dynamic LDS of k_extend<true>
 struct EhL {   // offset-based so the accesses stay in the LDS address space (ds_read/ds_write, not flat)
@@ -942,6 +948,11 @@ struct EhL {   // offset-based so the accesses stay in the LDS address space (ds
     bool *ovf = nullptr;
     DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + j * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
     DEV void set(int j, int2 v) const { g_lds_eh[base + j * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
+    using Cur = int;
+    DEV Cur cur(int j) const { return j; }
+    DEV Cur adv(Cur c) const { return c + 1; }
+    DEV int2 at(Cur c) const { return get(c); }
+    DEV void put(Cur c, int2 v) const { set(c, v); }
 };
 
 #define EXT_LDS_COLS 64   // ring columns (a power of two)
@@ -955,6 +966,21 @@ struct EhRing {
     int base;
     DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
     DEV void set(int j, int2 v) const { g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
+    // Cell-loop cursor: the slot's byte offset 4 * (lane + (j & 63) * 64) (base is the lane, < 64, and the ring is the
+    // first 16 KB of the dynamic LDS), advanced by one add and one and per column instead of recomputed for every
+    // access (the loop reads column j + 1 and stores column j: the store's slot is the previous read's).
+    using Cur = uint32_t;
+    DEV Cur cur(int j) const { return 4u * ((uint32_t)base + ((uint32_t)j & (EXT_LDS_COLS - 1)) * 64u); }
+    DEV Cur adv(Cur c) const { return (c + 256u) & (EXT_LDS_COLS * 256u - 1u); }
+    DEV int2 at(Cur c) const
+    {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(g_lds_eh) + c);
+        return make_int2((int)(v & 0xffffu), (int)(v >> 16));
+    }
+    DEV void put(Cur c, int2 v) const
+    {
+        *reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(g_lds_eh) + c) = (uint32_t)v.x | ((uint32_t)v.y << 16);
+    }
 };
 
 // Query accessors whose values are pre-scaled codes (4 * code) with readable padding one column past either
@@ -1016,11 +1042,13 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
         // stored h and e is >= 0, so "non-zero" is (h | e) != 0.
         int nzf = beg < end ? end : beg, nzl = -1;   // (the serial scan's start values)
         if (beg < end) {
-            int2 p = eh.get(beg);
+            typename EH::Cur cj = eh.cur(beg);
+            int2 p = eh.at(cj);
             int qj = query(beg);
 #pragma unroll 2   // two cells per trip: no loop-carried register copies, half the loop control (42 -> 36 per cell)
             for (j = beg; j < end; ++j) {
-                const int2 pn = eh.get(j + 1);
+                const typename EH::Cur cn = eh.adv(cj);
+                const int2 pn = eh.at(cn);
                 const int qn = pre ? query(j + 1) : (j + 1 < end ? query(j + 1) : 0);
                 int h, M = p.x, e = p.y;
                 const int hx = h1;
@@ -1033,11 +1061,11 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
                 m = m > h ? m : h;
                 t = M - oe_del; t = t > 0 ? t : 0;
                 e -= e_del; e = e > t ? e : t;
-                eh.set(j, make_int2(hx, e));
+                eh.put(cj, make_int2(hx, e));
                 if ((hx | e) != 0) { nzl = j; nzf = nzf < j ? nzf : j; }
                 t = M - oe_ins; t = t > 0 ? t : 0;
                 f -= e_ins; f = f > t ? f : t;
-                p = pn; qj = qn;
+                p = pn; qj = qn; cj = cn;
             }
         } else j = beg;
         eh.set(end, make_int2(h1, 0));
