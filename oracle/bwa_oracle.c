@@ -640,7 +640,8 @@ static void reverse_intvs(intv_v *p)
 #ifdef ORC_PROFILE
 /* seeding work profile (tools/seed_profile.py): bwt_extend calls by phase and by what the interval is
  * (the string fits the GPU k-mer table / the interval has one occurrence / other) */
-uint64_t orc_prof[16];   /* [12..15]: backward extensions of strings of 12..15 bases */
+uint64_t orc_prof[20];   /* [12..15]: backward extensions of strings of 12..15 bases; [16..19] ksw_extend2 rows, cells,
+                             rows and cells after the one-column tail condition (tools/ext_profile.py) */
 void orc_profile_get(uint64_t *out) { memcpy(out, orc_prof, sizeof orc_prof); }
 #define PROF(k) (++orc_prof[k])
 #else
@@ -894,6 +895,9 @@ static int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
     max = h0, max_i = max_j = -1; max_ie = -1, gscore = -1;
     max_off = 0;
     beg = 0, end = qlen;
+#ifdef ORC_PROFILE
+    int tail = 0, row_reached_qlen = 0;
+#endif
     for (i = 0; i < tlen; ++i) {
         int t, f = 0, h1, mm = 0, mj = -1;
         int8_t *q = &qp[target[i] * qlen];
@@ -921,6 +925,11 @@ static int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
             f -= e_ins; f = f > t ? f : t;
         }
         eh[end].h = h1; eh[end].e = 0;
+#ifdef ORC_PROFILE
+        row_reached_qlen = j == qlen;
+        PROF(16); orc_prof[17] += (uint64_t)(end > beg ? end - beg : 0);
+        if (tail) { PROF(18); orc_prof[19] += (uint64_t)(end > beg ? end - beg : 0); }
+#endif
         if (j == qlen) {
             max_ie = gscore > h1 ? max_ie : i;
             gscore = gscore > h1 ? gscore : h1;
@@ -940,6 +949,9 @@ static int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
         beg = j;
         for (j = end; j >= beg && eh[j].h == 0 && eh[j].e == 0; --j);
         end = j + 2 < qlen ? j + 2 : qlen;
+#ifdef ORC_PROFILE
+        if (!tail && qlen >= 2 && beg == qlen - 1 && end == qlen && eh[qlen - 1].h == 0 && row_reached_qlen) tail = 1;
+#endif
     }
     free(eh); free(qp);
     if (_qle) *_qle = max_j + 1;
