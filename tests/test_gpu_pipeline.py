@@ -117,12 +117,16 @@ def test_pipeline_fetches_equal_single_calls(setup, slots):
             assert cols == _columns(L, pi.handle, pi.options, fs, 500 + first), first
 
 
-@pytest.mark.parametrize("slots", [2, 4])
-def test_deferred_staging_fetches_equal_single_calls(setup, slots):
+@pytest.mark.parametrize("slots,run_cap", [(2, None), (4, None), (8, "2"), (6, "1")])
+def test_deferred_staging_fetches_equal_single_calls(setup, monkeypatch, slots, run_cap):
     """bsq_pipeline_submit_deferred (the drop-in's cursor loop since round 5, extension_bsq.cpp for_each_fetch_held):
     fetch k is staged by a pipeline worker; the caller frees its varlenas (here: overwrites them with other reads)
     only after submitting fetch k+1 and bsq_pipeline_wait_staged past k's ticket.  Every fetch's rows and columns
-    equal aligning it alone, tickets count submissions, and a fetch freed after its wait cannot change its rows."""
+    equal aligning it alone, tickets count submissions, and a fetch freed after its wait cannot change its rows.
+    With fewer concurrent alignments than slots (BSQ_PIPE_RUN) the slots share run_cap device workspace sets, lent
+    per alignment turn to fetches of different sizes (a set sized for 1 read grows for 6,000)."""
+    if run_cap:
+        monkeypatch.setenv("BSQ_PIPE_RUN", run_cap)
     pi, seqs = setup
     L = N.lib()
     sizes = [4000, 1, 0, 6000, 333, 5000, 2]
