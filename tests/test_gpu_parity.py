@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from bioseqdb_amd import synth
-from parity_util import build_pair, compare
+from parity_util import build_pair, compare, compare_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -167,3 +167,46 @@ def test_parity_chunked_batch(monkeypatch):
     rows, bad = compare(pi, oi, _texts(reads), first_call=5)
     assert rows > 2200
     assert not bad, bad[:20]
+
+
+def _revcomp(s):
+    return s[::-1].translate(str.maketrans("ACGTN", "TGCAN"))
+
+
+def _degenerate_reads(rows):
+    """Reads at the edges of mem_align1's input space, built from the reference rows."""
+    rng = random.Random(71)
+    a, b = rows[0], rows[1]
+    out = ["", "A", "AC", "ACGTACGTAC", a[1000:1018], a[2000:2019], a[3000:3020],   # empty, below / at min_seed_len
+           "N" * 150, "N" * 10 + a[5000:5140], a[6000:6140] + "N" * 10,           # all-N, N-padded
+           "A" * 150, "ACGT" * 37 + "AC",                                       # low complexity
+           _revcomp(a[7000:7150]), _revcomp(b[100:250]),                        # reverse strand
+           a[-75:] + b[:75],                                                    # across two reference rows
+           a[:150], b[-150:],                                                   # at the ends of the text
+           a[9000:9300], a[10000:10700]]                                        # longer reads
+    iupac = list(a[12000:12150])
+    for p in rng.sample(range(150), 6):
+        iupac[p] = rng.choice("RYKMSWBDHVN")
+    out.append("".join(iupac))
+    mm = list(a[13000:13150])
+    for p in range(5, 150, 9):   # a mismatch every 9 bases: no SMEM reaches min_seed_len
+        mm[p] = "ACGT"[("ACGT".index(mm[p]) + 1) % 4]
+    out.append("".join(mm))
+    return out
+
+
+def test_parity_degenerate_reads():
+    """Empty, one-base and sub-seed-length reads, all-N and N-padded reads, low-complexity, reverse-strand, reads
+    across two reference rows and at the text's ends, IUPAC symbols and a read without any seed: rows (and their
+    absence) equal the oracle's, one read at a time and as one batch."""
+    ref = synth.make_reference(300_000, n_rows=2, n_run_every=150_000, n_run_len=200)
+    rows = [t.decode() for t in ref.texts()]
+    reads = _degenerate_reads(rows)
+    pi, oi = build_pair(rows)
+    n_rows, bad = compare(pi, oi, reads, first_call=17)
+    assert n_rows >= 10
+    assert not bad, bad[:20]
+    from bioseqdb_amd import NucleotideSequence
+    n_rows2, bad2 = compare_batch(pi, oi, [NucleotideSequence.from_text(t) for t in reads], first_call=17)
+    assert n_rows2 == n_rows
+    assert not bad2, bad2[:20]
