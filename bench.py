@@ -968,6 +968,86 @@ def main() -> int:
     # ---- host materialisation: the last step's rows rendered as bwa_result text ----
     if rank == 0 and not cfg["seeding"] and n_hits and not args.timed_only:
         keep, ptrs = reads_as_nuclseq(L, reads)
+        # measured first, right after the timed steps: the renderers and the one-shot call below leave streams and
+        # pipelines in the process that a backend running this loop would not have
+        # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
+        # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (16) (each fetch staged, then its tuples released),
+        # the oldest fetch's rows taken when the pipeline is full; with the two nuclseq columns per row
+        # (build_tuple_bwa) rendered on the GPU, and without them
+        hb.phase = "pipelined cursor fetches"
+        fetch, depth, passes = 262144, args.cursor_depth, 4   # a 4M-read cursor: the batch's reads 4 times (16 fetches)
+
+        t_sub, sub_s = [0.0], [0.0]
+
+        def cursor(cols, deferred=True):
+            # deferred (the drop-in's loop since round 5, extension_bsq.cpp for_each_fetch_held): fetch k is staged by a
+            # pipeline worker, and its tuples are "freed" after fetch k+1 is submitted and k's staging has finished;
+            # copy: staged on the caller's thread inside bsq_pipeline_submit (round 4)
+            p = ctypes.c_void_p()
+            N.check(L.bsq_pipeline_create(idx, depth, ctypes.byref(p)))
+            try:
+                rows, best = 0, None
+                for rep in range(3):   # first pass allocates the slots' workspaces
+                    t_sub[0] = 0.0
+                    t1 = time.perf_counter()
+                    pend, rows, held = 0, 0, -1
+
+                    def take():
+                        v = ctypes.POINTER(N.Hits)()
+                        N.check(L.bsq_pipeline_next(p, ctypes.byref(v), None, None))
+                        N.check(L.bsq_pipeline_release(p))
+                        return int(v.contents.n_hits)
+                    for lo in [q * reads.n + x for q in range(passes) for x in range(0, reads.n, fetch)]:
+                        if pend == depth:
+                            rows += take()
+                            pend -= 1
+                        r0 = lo % reads.n
+                        n = min(fetch, reads.n - r0)
+                        sp = ctypes.cast(ctypes.addressof(ptrs) + r0 * ctypes.sizeof(ctypes.c_void_p), ctypes.c_void_p)
+                        t2 = time.perf_counter()
+                        if deferred:
+                            tk = ctypes.c_int64()
+                            N.check(L.bsq_pipeline_submit_deferred(p, ctypes.byref(opts), sp, n, first_call + lo, cols,
+                                                                   ctypes.byref(tk)))
+                            if held >= 0:
+                                N.check(L.bsq_pipeline_wait_staged(p, held + 1))
+                            held = tk.value
+                        else:
+                            N.check(L.bsq_pipeline_submit(p, ctypes.byref(opts), sp, n, first_call + lo, cols))
+                        t_sub[0] += time.perf_counter() - t2
+                        pend += 1
+                    if held >= 0:
+                        N.check(L.bsq_pipeline_wait_staged(p, held + 1))
+                    while pend:
+                        rows += take()
+                        pend -= 1
+                    dt = time.perf_counter() - t1
+                    if rep > 0 and (best is None or dt < best):
+                        best = dt
+                        sub_s[0] = t_sub[0]
+                return rows, best
+            finally:
+                L.bsq_pipeline_free(p)
+
+        rows_c, dt_c = cursor(1)
+        sub_c = sub_s[0]
+        rows_r, dt_r = cursor(0)
+        sub_r = sub_s[0]
+        rows_cc, dt_cc = cursor(1, deferred=False)
+        nr = passes * reads.n
+        result["sql_cursor"] = {
+            "reads": nr, "fetch_rows": fetch, "depth": depth,
+            "reads_per_s_with_columns": round(nr / dt_c, 1), "reads_per_s_records_only": round(nr / dt_r, 1),
+            "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits and rows_cc == passes * n_hits,
+            "submit_s": [round(sub_c, 4), round(sub_r, 4)], "loop_s": [round(dt_c, 4), round(dt_r, 4)],
+            "copy_staging_reads_per_s_with_columns": round(nr / dt_cc, 1),
+            "note": "bsq_pipeline over fetches of host nuclseq varlenas (deferred submissions: staged by the pipeline's "
+                    "workers while the caller submits the next fetch, then upload, alignment, D2H, and with columns the "
+                    "two nuclseq columns of every row on the GPU), as extension_bsq.cpp's cursor loop runs it, over a "
+                    "cursor of the batch's reads 4 times (lrand48 positions continuing); best of 2 runs after a warm-up "
+                    "run; copy_staging_*: the same with the staging on the caller's thread (round 4's loop)"}
+        # beside the headline: the drop-in's own call path (the pipelined cursor loop, columns included)
+        result["value_sql_call"] = round(nr / dt_c, 1)
         if not args.cursor_only:
             hb.phase = "rendering rows on the host"
             base = ctypes.addressof(ptrs)
@@ -1047,84 +1127,6 @@ def main() -> int:
             L.bsq_hits_free(ho)
             N.check(L.bsq_index_release_pool(idx))   # the one-shot call's workspaces (C4: ~60 GB of HBM)
 
-        # the cursor loop of nuclseq_multi_search_bwa as extension_bsq.cpp runs it: fetches of BSQ_FETCH_ROWS
-        # (262144) reads submitted to a bsq_pipeline of depth --cursor-depth (16) (each fetch staged, then its tuples released),
-        # the oldest fetch's rows taken when the pipeline is full; with the two nuclseq columns per row
-        # (build_tuple_bwa) rendered on the GPU, and without them
-        hb.phase = "pipelined cursor fetches"
-        fetch, depth, passes = 262144, args.cursor_depth, 4   # a 4M-read cursor: the batch's reads 4 times (16 fetches)
-
-        t_sub, sub_s = [0.0], [0.0]
-
-        def cursor(cols, deferred=True):
-            # deferred (the drop-in's loop since round 5, extension_bsq.cpp for_each_fetch_held): fetch k is staged by a
-            # pipeline worker, and its tuples are "freed" after fetch k+1 is submitted and k's staging has finished;
-            # copy: staged on the caller's thread inside bsq_pipeline_submit (round 4)
-            p = ctypes.c_void_p()
-            N.check(L.bsq_pipeline_create(idx, depth, ctypes.byref(p)))
-            try:
-                rows, best = 0, None
-                for rep in range(3):   # first pass allocates the slots' workspaces
-                    t_sub[0] = 0.0
-                    t1 = time.perf_counter()
-                    pend, rows, held = 0, 0, -1
-
-                    def take():
-                        v = ctypes.POINTER(N.Hits)()
-                        N.check(L.bsq_pipeline_next(p, ctypes.byref(v), None, None))
-                        N.check(L.bsq_pipeline_release(p))
-                        return int(v.contents.n_hits)
-                    for lo in [q * reads.n + x for q in range(passes) for x in range(0, reads.n, fetch)]:
-                        if pend == depth:
-                            rows += take()
-                            pend -= 1
-                        r0 = lo % reads.n
-                        n = min(fetch, reads.n - r0)
-                        sp = ctypes.cast(ctypes.addressof(ptrs) + r0 * ctypes.sizeof(ctypes.c_void_p), ctypes.c_void_p)
-                        t2 = time.perf_counter()
-                        if deferred:
-                            tk = ctypes.c_int64()
-                            N.check(L.bsq_pipeline_submit_deferred(p, ctypes.byref(opts), sp, n, first_call + lo, cols,
-                                                                   ctypes.byref(tk)))
-                            if held >= 0:
-                                N.check(L.bsq_pipeline_wait_staged(p, held + 1))
-                            held = tk.value
-                        else:
-                            N.check(L.bsq_pipeline_submit(p, ctypes.byref(opts), sp, n, first_call + lo, cols))
-                        t_sub[0] += time.perf_counter() - t2
-                        pend += 1
-                    if held >= 0:
-                        N.check(L.bsq_pipeline_wait_staged(p, held + 1))
-                    while pend:
-                        rows += take()
-                        pend -= 1
-                    dt = time.perf_counter() - t1
-                    if rep > 0 and (best is None or dt < best):
-                        best = dt
-                        sub_s[0] = t_sub[0]
-                return rows, best
-            finally:
-                L.bsq_pipeline_free(p)
-
-        rows_c, dt_c = cursor(1)
-        sub_c = sub_s[0]
-        rows_r, dt_r = cursor(0)
-        sub_r = sub_s[0]
-        rows_cc, dt_cc = cursor(1, deferred=False)
-        nr = passes * reads.n
-        result["sql_cursor"] = {
-            "reads": nr, "fetch_rows": fetch, "depth": depth,
-            "reads_per_s_with_columns": round(nr / dt_c, 1), "reads_per_s_records_only": round(nr / dt_r, 1),
-            "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits and rows_cc == passes * n_hits,
-            "submit_s": [round(sub_c, 4), round(sub_r, 4)], "loop_s": [round(dt_c, 4), round(dt_r, 4)],
-            "copy_staging_reads_per_s_with_columns": round(nr / dt_cc, 1),
-            "note": "bsq_pipeline over fetches of host nuclseq varlenas (deferred submissions: staged by the pipeline's "
-                    "workers while the caller submits the next fetch, then upload, alignment, D2H, and with columns the "
-                    "two nuclseq columns of every row on the GPU), as extension_bsq.cpp's cursor loop runs it, over a "
-                    "cursor of the batch's reads 4 times (lrand48 positions continuing); best of 2 runs after a warm-up "
-                    "run; copy_staging_*: the same with the staging on the caller's thread (round 4's loop)"}
-        # beside the headline: the drop-in's own call path (the pipelined cursor loop, columns included)
-        result["value_sql_call"] = round(nr / dt_c, 1)
         del keep, ptrs
 
     # ---- bulk codec: the reference rows through nuclseq_in on the GPU vs the
