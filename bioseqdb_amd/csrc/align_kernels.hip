@@ -2105,44 +2105,63 @@ hipError_t launch_chain(int grid, hipStream_t st, const DIndex &ix, const DOpts 
     return hipGetLastError();
 }
 
-// Sort key of a read for the extension stage: its number of chains, then the estimated DP work (the query
-// bases outside each chain's longest seed, summed over chains: ksw_extend2 runs ~one row per such base).
+// Sort key of a read for the extension stage: its number of chains, then the number of sides its first extended seed
+// (the first chain's top seed in mem_chain2aln's order: largest score, then largest index) extends to, then that
+// seed's left extent in 8-base buckets, then the estimated DP work (the query bases outside each chain's longest
+// seed, summed over chains: ksw_extend2 runs ~one row per such base).
 // Ordering by chain count first cut k_extend from 10.4 to 8.6 ms per 1M C3 reads (ordering by the DP estimate
-// alone, or by chains, then seeds, then the estimate, left lanes of a wave in different seed loops).
+// alone, or by chains, then seeds, then the estimate, left lanes of a wave in different seed loops).  The sides
+// (round 5): mem_chain2aln's left and right extensions are two loops one after the other, each as long as its
+// longest lane, so a wave mixing reads extended only to the left with reads extended only to the right (or on both
+// sides) runs both loops at full length with half the lanes idle in each.  The left extent keeps left-only reads
+// (extent >= 8) apart from right-only ones (0) and orders the two-sided reads' left calls; the estimate then orders
+// the rest by rows.  tools/ext_model.py (the oracle's per-row trace of 4,096 C3 reads) puts this key at 0.72 of the
+// previous one's lockstep time; lone 1M-read C3 launches measured extension 5.50 -> 4.70-4.82 ms, C4 76.1 -> 63.4 ms
+// (profiles/r05/ext_key/).  Keyed instead by which sides (left only / right only / both) and the longer extent in
+// 4-base buckets (model 0.67): 4.92-4.95 ms at C3, 62.2 ms at C4 -- not kept.
 __global__ void k_ext_key(const Caps cp, const int64_t *__restrict__ offs, const int32_t *__restrict__ sel, int n,
                           const ChainDesc *__restrict__ chains, const Seed *__restrict__ seeds,
                           const int32_t *__restrict__ n_chains, const uint32_t *__restrict__ status,
-                          uint32_t *__restrict__ key, int32_t *__restrict__ idx)
+                          const int32_t *__restrict__ sscore, uint32_t *__restrict__ key, int32_t *__restrict__ idx)
 {
     const int li = blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= n) return;
-    uint32_t est = 0;
+    uint32_t est = 0, sides = 0, lb = 0;
     if (!status[li]) {
         const int r = read_of(sel, li);
         const int len = (int)(offs[r + 1] - offs[r]);
         const ChainDesc *cd = chains + (size_t)li * cp.chains;
         const Seed *sd = seeds + (size_t)li * cp.seeds;
+        const int32_t *ss = sscore ? sscore + (size_t)li * cp.seeds : nullptr;
         const int nc = n_chains[li];
         for (int c = 0; c < nc; ++c) {
             int best = 0;
             for (int k = 0; k < cd[c].n; ++k) best = best > sd[cd[c].seed_off + k].len ? best : sd[cd[c].seed_off + k].len;
             est += (uint32_t)(len > best ? len - best : 0) + 4u;
         }
+        if (nc > 0 && cd[0].n > 0) {
+            int top = 0, ts = -1;
+            for (int k = 0; k < cd[0].n; ++k) {   // seed_order's last entry: (score, index) largest
+                const int sc = ss ? ss[cd[0].seed_off + k] : sd[cd[0].seed_off + k].len;
+                if (sc >= ts) { ts = sc; top = k; }
+            }
+            const Seed &s = sd[cd[0].seed_off + top];
+            sides = (uint32_t)(s.qbeg > 0) + (uint32_t)(s.qbeg + s.len != len);
+            lb = (uint32_t)(s.qbeg >> 3) < 63u ? (uint32_t)(s.qbeg >> 3) : 63u;
+        }
     }
-    // primary: the number of chains (each one is a pass of mem_chain2aln's seed loop, the main source of
-    // divergence between the lanes of a wave); secondary: the DP estimate
     const uint32_t nc2 = status[li] ? 0u : (uint32_t)(n_chains[li] < 63 ? n_chains[li] : 63);
-    key[li] = nc2 << 18 | (est < 262143u ? est : 262143u);
+    key[li] = nc2 << 24 | sides << 22 | lb << 16 | (est < 65535u ? est : 65535u);
     idx[li] = li;
 }
 
 hipError_t launch_ext_key(hipStream_t st, const Caps &cp, const int64_t *offs, const int32_t *sel, int n,
                           const ChainDesc *chains, const Seed *seeds, const int32_t *n_chains, const uint32_t *status,
-                          uint32_t *key, int32_t *idx)
+                          const int32_t *sscore, uint32_t *key, int32_t *idx)
 {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ext_key, dim3((n + 255) / 256), dim3(256), 0, st, cp, offs, sel, n, chains, seeds, n_chains,
-                       status, key, idx);
+                       status, sscore, key, idx);
     return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@ hipError_t launch_flt_seeds(int, hipStream_t, const DIndex &, const DOpts &, con
                             const int32_t *, int, ChainDesc *, Seed *, const int32_t *, const uint32_t *, int32_t *,
                             uint8_t *, Counters *);
 hipError_t launch_ext_key(hipStream_t, const Caps &, const int64_t *, const int32_t *, int, const ChainDesc *,
-                          const Seed *, const int32_t *, const uint32_t *, uint32_t *, int32_t *);
+                          const Seed *, const int32_t *, const uint32_t *, const int32_t *, uint32_t *, int32_t *);
 hipError_t launch_reg2aln(int, hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *,
                           const int32_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *, uint32_t *,
                           uint8_t *, Counters *);
@@ -857,7 +857,7 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.eidx0, R * 4));
         HIPCHK(hipMalloc(&w.eidx1, R * 4));
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, w.esort_bytes, w.ekey0, w.ekey1, w.eidx0, w.eidx1, (int)R,
-                                                  0, 24));   // the widest key sorted (the extension's, 24 bits)
+                                                  0, 30));   // the widest key sorted (the extension's, 30 bits)
         HIPCHK(hipMalloc(&w.esort_tmp, std::max<size_t>(w.esort_bytes, 16)));
     }
     return BSQ_OK;
@@ -1389,9 +1389,10 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
     const int32_t *order = nullptr;
     if (!sel && w.ekey0 && n > 0) {
         // lane balance: run the extension in order of estimated DP work so each wave holds similar reads
-        HIPCHK(launch_ext_key(st, w.cp, (b->offs + b->lo), sel, n, w.chains, w.seeds, w.n_chains, w.status, w.ekey0, w.eidx0));
+        HIPCHK(launch_ext_key(st, w.cp, (b->offs + b->lo), sel, n, w.chains, w.seeds, w.n_chains, w.status, w.sscore,
+                              w.ekey0, w.eidx0));
         size_t tb = w.esort_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 24, st));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 30, st));
         order = w.eidx1;
     }
     HIPCHK(launch_extend(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, (b->ids + b->lo), n, w.chains, w.seeds, w.n_chains, w.regs,

@@ -898,6 +898,9 @@ static int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
 #ifdef ORC_PROFILE
     int tail = 0, row_reached_qlen = 0;
 #endif
+#ifdef ORC_PROFILE
+    tr_push(10, qlen, tlen, w);
+#endif
     for (i = 0; i < tlen; ++i) {
         int t, f = 0, h1, mm = 0, mj = -1;
         int8_t *q = &qp[target[i] * qlen];
@@ -928,6 +931,7 @@ static int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
 #ifdef ORC_PROFILE
         row_reached_qlen = j == qlen;
         PROF(16); orc_prof[17] += (uint64_t)(end > beg ? end - beg : 0);
+        tr_push(11, end > beg ? end - beg : 0, beg, end);
         if (tail) { PROF(18); orc_prof[19] += (uint64_t)(end > beg ? end - beg : 0); }
 #endif
         if (j == qlen) {
@@ -1470,6 +1474,9 @@ static void mem_chain2aln(const mopt_t *opt, const orc_index *bns, int l_query, 
     }
     rseq = bns_fetch_seq(bns, &rmax[0], c->seeds[0].rbeg, &rmax[1], &rid);
     srt = malloc((size_t)c->n * 8);
+#ifdef ORC_PROFILE
+    tr_push(20, c->n, (int)max, 0);
+#endif
     for (i = 0; i < c->n; ++i) srt[i] = (uint64_t)c->seeds[i].score << 32 | (uint64_t)i;
     ks_introsort((size_t)c->n, srt, 8, u64_lt);
     for (k = c->n - 1; k >= 0; --k) {
@@ -1498,8 +1505,16 @@ static void mem_chain2aln(const mopt_t *opt, const orc_index *bns, int l_query, 
                 if (s->qbeg <= t->qbeg && s->qbeg + s->len - t->qbeg >= s->len >> 2 && t->qbeg - s->qbeg != t->rbeg - s->rbeg) break;
                 if (t->qbeg <= s->qbeg && t->qbeg + t->len - s->qbeg >= s->len >> 2 && s->qbeg - t->qbeg != s->rbeg - t->rbeg) break;
             }
-            if (i == c->n) { srt[k] = 0; continue; }
+            if (i == c->n) {
+#ifdef ORC_PROFILE
+                tr_push(21, 1, 0, 0);
+#endif
+                srt[k] = 0; continue;
+            }
         }
+#ifdef ORC_PROFILE
+        tr_push(21, 0, s->qbeg, s->len);
+#endif
         VGROW(*av);
         a = &av->a[av->n++];
         memset(a, 0, sizeof(mem_alnreg_t));
@@ -1512,6 +1527,9 @@ static void mem_chain2aln(const mopt_t *opt, const orc_index *bns, int l_query, 
             qs = malloc((size_t)s->qbeg);
             for (i = 0; i < s->qbeg; ++i) qs[i] = query[s->qbeg - 1 - i];
             tmp = s->rbeg - rmax[0];
+#ifdef ORC_PROFILE
+            tr_push(22, 0, 0, 0);
+#endif
             rs = malloc(tmp > 0 ? (size_t)tmp : 1);
             for (i = 0; i < tmp; ++i) rs[i] = rseq[tmp - 1 - i];
             for (i = 0; i < MAX_BAND_TRY; ++i) {
@@ -1534,6 +1552,9 @@ static void mem_chain2aln(const mopt_t *opt, const orc_index *bns, int l_query, 
             int qle, tle, qe, re, gtle, gscore, sc0 = a->score;
             qe = s->qbeg + s->len;
             re = (int)(s->rbeg + s->len - rmax[0]);
+#ifdef ORC_PROFILE
+            tr_push(22, 1, 0, 0);
+#endif
             for (i = 0; i < MAX_BAND_TRY; ++i) {
                 int prev = a->score;
                 aw[1] = opt->w << i;
@@ -1906,6 +1927,22 @@ int orc_seed_trace(const orc_index *idx, const orc_opts *o, const uint8_t *q, in
     orc_tr = out; orc_tr_n = 0; orc_tr_cap = cap;
     uint64_t tmp[4 * 512];
     orc_collect_intv(idx, o, q, len, tmp, 512);
+    const int n = orc_tr_n;
+    orc_tr = NULL; orc_tr_n = 0; orc_tr_cap = 0;
+    return n;
+}
+
+/* The extension trace of one read (ORC_PROFILE builds only; tools/ext_model.py): 4 int32 per record {20, seeds, longest
+ * seed} per mem_chain2aln call, {21, skipped, qbeg, len} per seed it
+ * visits (qbeg and len for extended seeds), {22, side} per extension side (0 left, 1 right), {10, qlen,
+ * tlen, w} per ksw_extend2 call and {11, cells, beg, end} per row of it; returns the number of int32 written. */
+int orc_ext_trace(const orc_index *idx, const orc_opts *o, const uint8_t *q, int len, int64_t id, int32_t *out, int cap)
+{
+    orc_tr = out; orc_tr_n = 0; orc_tr_cap = cap;
+    mopt_t opt; make_opt(o, &opt);
+    alnreg_v regs = {0, 0, 0};
+    if (idx->built) mem_align1(&opt, idx, len, q, id, &regs);
+    free(regs.a);
     const int n = orc_tr_n;
     orc_tr = NULL; orc_tr_n = 0; orc_tr_cap = 0;
     return n;

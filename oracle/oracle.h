@@ -104,6 +104,7 @@ int orc_align_regions(const orc_index *idx, const orc_opts *opt, const uint8_t *
 int orc_collect_intv(const orc_index *idx, const orc_opts *opt, const uint8_t *q_nt4, int len, uint64_t *out, int max);
 /* Seeding trace of one read for tools/seed_model.py (bwa_oracle.c tr_push); test infrastructure. */
 int orc_seed_trace(const orc_index *idx, const orc_opts *o, const uint8_t *q, int len, int32_t *out, int cap);
+int orc_ext_trace(const orc_index *idx, const orc_opts *o, const uint8_t *q, int len, int64_t id, int32_t *out, int cap);
 
 /* Bench helper: aligns n reads (nt4 codes, concatenated, offsets[n+1]) with `threads` POSIX threads,
  * returning the number of regions and a 64-bit FNV checksum of (read, rb, re, qb, qe, score, flag,

@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU box (round 5): extension sort key with the first seed's sides and left extent -- alignment tests on the new
+# library, then C3 / C2 (full-batch checksums) alternating with the previous build (BSQ_LIB=tools/bin/libbsq_base.so),
+# two rounds, and C4 once each.
+tag=${1:-extkey}
+mkdir -p gpurun_out/$tag
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_golden.py tests/test_gpu_configs.py tests/test_gpu_pipeline.py > gpurun_out/$tag/tests.log 2>&1
+rc=$?; tail -3 gpurun_out/$tag/tests.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do for v in base new; do
+  if [ $v = base ]; then export BSQ_LIB=$PWD/tools/bin/libbsq_base.so; else unset BSQ_LIB; fi
+  timeout -k 10 300 python -u bench.py --timed-only --checksums > gpurun_out/$tag/c3_${v}_$rep.json 2>> gpurun_out/$tag/ab.err || exit 1
+  python3 -c "import json; d=json.load(open('gpurun_out/$tag/c3_${v}_$rep.json')); print('c3 $v', d['value'], d['ms_per_step'], {k: v['ms'] for k, v in d['kernels'].items()}, d['checksums'])"
+  timeout -k 10 300 python -u bench.py --config c2 --timed-only --checksums > gpurun_out/$tag/c2_${v}_$rep.json 2>> gpurun_out/$tag/ab.err || exit 1
+  python3 -c "import json; d=json.load(open('gpurun_out/$tag/c2_${v}_$rep.json')); print('c2 $v', d['value'], d['ms_per_step'], d['checksums'])"
+done; done
+for v in base new; do
+  if [ $v = base ]; then export BSQ_LIB=$PWD/tools/bin/libbsq_base.so; else unset BSQ_LIB; fi
+  timeout -k 10 600 python -u bench.py --config c4 --timed-only --checksums > gpurun_out/$tag/c4_${v}.json 2>> gpurun_out/$tag/ab.err || exit 1
+  python3 -c "import json; d=json.load(open('gpurun_out/$tag/c4_${v}.json')); print('c4 $v', d['value'], d['ms_per_step'], {k: v['ms'] for k, v in d['kernels'].items()}, d['checksums'])"
+done
