@@ -51,8 +51,7 @@ from bioseqdb_amd import _native as N  # noqa: E402
 METRIC = "aligned reads/sec (150 bp vs 100 Mbp ref) at 1/2/4/8 MI355X; bit-exact vs libbwa"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # stage -> the main-pass kernel its HIP events bracket (libbsq run_stages)
-STAGE_KERNEL = {"smem": ("k_codes_wave+k_smem_lanes" if os.environ.get("BSQ_SMEM_LANES") == "1"
-                         else "k_codes_wave+k_smem_lds"),   # BSQ_SMEM_LANES=1: persistent lanes (smem.hip)
+STAGE_KERNEL = {"smem": "k_codes_wave+k_smem_lds",
                 "chain": "k_chain_s+k_chain", "extend": "k_ext_key+sort+k_extend",
                 "reg2aln": "k_r2a_key+sort+k_reg2aln_diag+g16+g32+w"}
 # per-launch HBM traffic from the committed PMC passes (tools/profile_round.sh + tools/traffic_from_pmc.py,

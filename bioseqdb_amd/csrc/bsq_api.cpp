@@ -62,10 +62,6 @@ bool wide_z32(const DIndex &);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
-int sm_words(int);
-bool sm_applies(const DIndex &, int);
-hipError_t launch_smem_sm(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
-                          Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint32_t *, int);
 struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
 struct RenderView {
     const bsq_hit *hits; const uint32_t *cigar; int64_t n_hits; const uint8_t *pac; int64_t l_pac;
@@ -763,7 +759,6 @@ struct Workspace {
     int32_t *dlist0 = nullptr, *dlist1 = nullptr, *dcount = nullptr;   // reads deferred by the group kernels
     uint8_t *lspill = nullptr;   // SMEM list entries beyond the LDS share (main pass), LSPILL per read
     uint8_t *codes_t = nullptr;  // wave-transposed read codes for the main-pass seeding kernel (reads <= 1024 bases)
-    uint32_t *qpack = nullptr;   // k_smem_sm's packed reads (2-bit codes + hole bitmap + length; reads <= 320 bases)
     uint32_t *ekey0 = nullptr, *ekey1 = nullptr;   // extension work keys (main pass) and their sort
     int32_t *eidx0 = nullptr, *eidx1 = nullptr;
     void *esort_tmp = nullptr;
@@ -775,7 +770,7 @@ struct Workspace {
         hipFree(chains); hipFree(seeds); hipFree(regs); hipFree(hits); hipFree(cigars); hipFree(scratch); hipFree(sel);
         hipFree(sscore);
         hipFree(zslab); hipFree(dlist0); hipFree(dlist1); hipFree(dcount);
-        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill); hipFree(codes_t); hipFree(qpack);
+        hipFree(ekey0); hipFree(ekey1); hipFree(eidx0); hipFree(eidx1); hipFree(esort_tmp); hipFree(lspill); hipFree(codes_t);
         *this = Workspace{};
     }
 };
@@ -851,7 +846,6 @@ int ws_alloc(Workspace &w, const Caps &cp, int32_t max_reads, int workers, int64
         HIPCHK(hipMalloc(&w.dcount, 32));   // launch_reg2aln_chain's 5 counters, then k_extend's work counter
         HIPCHK(hipMalloc(&w.lspill, (size_t)intv_slot_reads((int64_t)R) * LSPILL * (2 * 8 + 4)));   // whole waves
         if (cp.max_len <= 1024) HIPCHK(hipMalloc(&w.codes_t, (size_t)intv_slot_reads((int64_t)R) * (size_t)cp.max_len));
-        if (cp.max_len <= 320) HIPCHK(hipMalloc(&w.qpack, R * (size_t)sm_words(cp.max_len) * 4));
         HIPCHK(hipMalloc(&w.ekey0, R * 4));
         HIPCHK(hipMalloc(&w.ekey1, R * 4));
         HIPCHK(hipMalloc(&w.eidx0, R * 4));
@@ -873,7 +867,6 @@ DOpts make_dopts(const bsq_opts &o)
     d.max_mem_intv = 20; d.split_factor = 1.5f; d.mask_level = 0.50f; d.drop_ratio = 0.50f; d.mask_level_redun = 0.95f;
     // mem_opt_init fills mat with a=1, b=4 and bioseqdb never refills it (Q2)
     d.mat_match = 1; d.mat_mismatch = -4; d.mat_amb = -1; d.mat_max = 1;
-    { const char *e = getenv("BSQ_SS_WALK"); d.ss_walk = e && *e == '1'; }
     return d;
 }
 
@@ -1327,14 +1320,6 @@ extern "C" int bsq_batch_set_nuclseqs(bsq_batch *b, const void *const *reads, in
     return batch_upload_staged(b, b->stage, true);
 }
 
-static int env_int(const char *name, int dflt)
-{
-    const char *v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
-// BSQ_SMEM_SM=1: the per-lane state-machine seeding kernel (smem.hip k_smem_sm) for u32 rows -- exact, but measured
-// 8x slower than k_smem_lds, so an experiment only
-static bool sm_enabled() { return env_int("BSQ_SMEM_SM", 0) != 0; }
 
 // Runs smem -> chain -> extend -> reg2aln on workspace w for n local reads.
 // Seeding (mem_collect_intv) on workspace w: the main-pass LDS kernel, or the large-capacity kernel for
@@ -1352,14 +1337,6 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         // 29.0 at 11, 30.4 at 10).  BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested
         // (tests/test_gpu_parity.py).
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
-        if (w.qpack && sm_applies(ix, w.cp.max_len) && sm_enabled()) {
-            // u32 rows, reads <= 320 bases: the per-lane state machine (smem.hip k_smem_sm), 14 list entries in LDS
-            // beside the packed read (13 KB per one-wave block, 12 waves per CU)
-            const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : env_int("BSQ_SM_LCAP", 14);
-            HIPCHK(launch_smem_sm(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
-                                  w.lspill, tiny_caps() ? 0 : LSPILL, w.qpack, env_int("BSQ_SM_RPL", 4)));
-            return BSQ_OK;
-        }
         const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : wide_z32(ix) ? 14 : 12;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));

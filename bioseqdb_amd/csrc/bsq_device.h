@@ -81,7 +81,6 @@ struct DOpts {
     int32_t min_seed_len, max_occ, split_width, max_chain_gap, min_chain_weight, max_chain_extend, max_mem_intv;
     float split_factor, mask_level, drop_ratio, mask_level_redun;
     int32_t mat_match, mat_mismatch, mat_amb, mat_max;   // the 5x5 matrix from bwa_fill_scmat (Q2)
-    int32_t ss_walk;     // bwt_seed_strategy1 on unique intervals by the text walk (BSQ_SS_WALK=0: one bwt_extend per base)
 };
 
 // Per-batch capacities (the main pass uses small ones; overflowing reads are re-run with large ones).

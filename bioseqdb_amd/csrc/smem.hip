@@ -520,230 +520,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
 }
 
 template <typename X, typename Z, typename Q>
-DEV int smem1_merged(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S,
-                  bool &ovf, uint64_t &nblk, uint64_t &nkm)
-{
-    S.n1 = 0;
-    if (q[x] > 3) return x + 1;
-    if (min_intv < 1) min_intv = 1;
-    int c0 = q[x];
-    X ik0 = fm.L2(c0) + 1, ik1 = fm.L2(3 - c0) + 1;
-    Z ik2 = (Z)(fm.L2(c0 + 1) - fm.L2(c0));
-    int ikend = x + 1;
-    int n = 0, i = x + 1;
-    uint32_t fcode = (uint32_t)c0;   // code of q[x..i] while i - x + 1 <= K
-    bool stop = false;               // the forward walk ended early (hole or interval below min_intv)
-    {
-        // Lengths 2..min(K, len - x) come from the k-mer table.  Their table rows depend only on the read's
-        // bases, so every row is loaded before the first one is used (one round trip instead of K - 1);
-        // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
-        // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
-        // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
-        // rows preloaded: 11, or 13 for 64-bit rows (whose table is 13 deep: C4); a deeper table (kmer_depth up to
-        // 15) serves lengths KM+1..K one per step below
-        constexpr int KM = sizeof(X) == 8 ? 13 : 11;
-        const int Kp = fm.K < KM ? fm.K : KM;
-        const int Lt = Kp < len - x ? Kp : len - x;
-        int cb[KM + 1];
-#pragma unroll
-        for (int t = 2; t <= KM; ++t) cb[t] = t <= Lt ? q[x + t - 1] : 4;
-        X e0[KM + 1];
-        Z e2[KM + 1];
-        int nt = 1;   // bases from x covered without a hole (capped at Lt)
-#pragma unroll
-        for (int t = 2; t <= KM; ++t) {
-            if (nt == t - 1 && cb[t] < 4) {
-                fcode = fcode << 2 | (uint32_t)cb[t];
-                fm.kget02(koff(t) + fcode, e0[t], e2[t]);
-                nt = t;
-            }
-        }
-        if (nt >= 2) {
-            nkm += (uint64_t)(nt - 1);
-            const X x1_last = fm.kget1(koff(nt) + fcode);
-#pragma unroll
-            for (int t = 2; t <= KM; ++t) {
-                if (t <= nt && !stop) {
-                    const X n0 = e0[t];
-                    const Z n2 = e2[t];
-                    if (n2 != ik2) {
-                        if (n >= L.total()) { ovf = true; return len; }
-                        L.set(n++, ik0, ik2, ikend);
-                        if (n2 < (Z)min_intv) { stop = true; i = x + t - 1; }
-                    }
-                    if (!stop) { ik0 = n0; ik2 = n2; ikend = x + t; }
-                }
-            }
-            ik1 = x1_last;
-        }
-        if (!stop) {
-            i = x + nt;
-            if (nt < Lt) {   // q[x + nt] is a hole: the walk stops there
-                if (n >= L.total()) { ovf = true; return len; }
-                L.set(n++, ik0, ik2, ikend);
-                stop = true;
-            }
-        }
-    }
-    int qi = !stop && i < len ? q[i] : 0;
-    // One loop for both phases of bwt_smem1: a lane that has finished its forward walk (reversed its list and set up
-    // the backward pass) takes its backward pairs in the same trips in which other lanes of the wave still extend
-    // forward, instead of waiting at the forward loop's exit for the wave's longest forward walk.  Per lane every
-    // step, and the order of the steps, is smem1_lds's.
-    const int K = fm.K;
-    int phase = 0;   // 0 forward, 1 backward, 2 done
-    int ret = 0, last_start = 0x7fffffff, c = -1, nc = 0, j = 0;
-    uint32_t wcode = 0;
-    Z last_x2 = 0;
-    for (;;) {
-        if (phase == 0) {
-            bool fend = stop || i >= len;
-            if (!fend) {
-                if (ik2 == 1 && min_intv <= 1) {   // the unique-interval text walk (smem1_lds)
-                    const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
-                    int k = i;
-                    for (;;) {
-                        constexpr int W = 8;
-                        int qc[W], tc[W];
-#pragma unroll
-                        for (int t = 0; t < W; ++t) {
-                            const bool in = k + t < len && p + k + t < nT;
-                            qc[t] = in ? q[k + t] : 5;
-                            tc[t] = in ? fm.tbase(p + k + t) : 4;
-                        }
-                        int r = W;
-#pragma unroll
-                        for (int t = W - 1; t >= 0; --t)
-                            if (qc[t] != tc[t]) r = t;
-                        k += r;
-                        if (r < W) break;
-                    }
-                    ikend = k;
-                    i = k;
-                    if (k < len) {
-                        if (n >= L.total()) { ovf = true; return len; }
-                        L.set(n++, ik0, ik2, ikend);
-                    }
-                    fend = true;
-                } else {
-                    const int cur = qi;
-                    qi = i + 1 < len ? q[i + 1] : 0;
-                    if (cur < 4) {
-                        const int cc = 3 - cur;
-                        X n1, n0;
-                        Z n2;
-                        fcode = fcode << 2 | (uint32_t)cur;
-                        if (i - x + 1 <= fm.K) {
-                            fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
-                            ++nkm;
-                        } else extend1(fm, ik1, ik0, ik2, cc, n1, n0, n2, nblk);
-                        if (n2 != ik2) {
-                            if (n >= L.total()) { ovf = true; return len; }
-                            L.set(n++, ik0, ik2, ikend);
-                            if (n2 < (Z)min_intv) fend = true;
-                        }
-                        if (!fend) {
-                            ik0 = n0; ik1 = n1; ik2 = n2; ikend = i + 1;
-                            if (++i >= len) fend = true;
-                        }
-                    } else {
-                        if (n >= L.total()) { ovf = true; return len; }
-                        L.set(n++, ik0, ik2, ikend);
-                        fend = true;
-                    }
-                }
-            }
-            if (fend) {   // the forward walk is over: last push, reversal, backward set-up
-                if (i == len) {
-                    if (n >= L.total()) { ovf = true; return len; }
-                    L.set(n++, ik0, ik2, ikend);
-                }
-                for (int jj = 0; jj < (n >> 1); ++jj) {
-                    X a0, b0;
-                    Z a2, b2;
-                    int ae, be;
-                    L.get(jj, a0, a2, ae);
-                    L.get(n - 1 - jj, b0, b2, be);
-                    L.set(jj, b0, b2, be);
-                    L.set(n - 1 - jj, a0, a2, ae);
-                }
-                { X d0; Z d2; L.get(0, d0, d2, ret); }
-                for (int t = 0; t < K; ++t) wcode = wcode << 2 | (x + t < len ? (uint32_t)(q[x + t] & 3) : 0u);
-                i = x - 1;
-                c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
-                if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
-                phase = 1;
-            }
-        }
-        if (phase == 1) {   // one pair of the flat backward loop (smem1_lds)
-            const bool hb = j + 1 < n;
-            X pa0, pb0;
-            Z pa2, pb2;
-            int pae, pbe;
-            L.get(j, pa0, pa2, pae);
-            L.get(hb ? j + 1 : j, pb0, pb2, pbe);
-            X oa0 = 0, ob0 = 0;
-            Z oa2 = 0, ob2 = 0;
-            if (c >= 0) {
-                const int La = pae - i, Lb = pbe - i;
-                const bool ta = La <= K, tb = hb && Lb <= K;
-                X ea0 = 0, eb0 = 0;
-                Z ea2 = 0, eb2 = 0;
-                if (ta) fm.kget02(koff(La) + (wcode >> (2 * (K - La))), ea0, ea2);
-                if (tb) fm.kget02(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb2);
-                nkm += (uint64_t)ta + (uint64_t)tb;
-                if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
-                if (ta) { oa0 = ea0; oa2 = ea2; }
-                if (tb) { ob0 = eb0; ob2 = eb2; }
-            }
-            for (int h = 0; h < 2; ++h) {
-                if (h == 1 && !hb) break;
-                const X p0 = h ? pb0 : pa0, o0 = h ? ob0 : oa0;
-                const Z p2 = h ? pb2 : pa2, o2 = h ? ob2 : oa2;
-                const int pe = h ? pbe : pae;
-                const bool keep_hit = c < 0 || o2 < (Z)min_intv;
-                if (keep_hit) {
-                    if (nc == 0 && (S.n1 == 0 || i + 1 < last_start)) {
-                        if (S.n + S.n1 >= S.cap) { ovf = true; return len; }
-                        Intv &m = S.a[S.cap - 1 - S.n1];
-                        m.x[0] = p0; m.x[1] = 0; m.x[2] = p2;
-                        m.info = (uint64_t)(uint32_t)(i + 1) << 32 | (uint32_t)pe;
-                        ++S.n1;
-                        last_start = i + 1;
-                    }
-                } else if (nc == 0 || o2 != last_x2) {
-                    L.set(nc++, o0, o2, pe);
-                    last_x2 = o2;
-                }
-            }
-            j += 2;
-            if (j >= n) {
-                if (nc == 0) phase = 2;
-                else {
-                    n = nc; nc = 0; j = 0; last_x2 = 0;
-                    --i;
-                    c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
-                    if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
-                }
-            }
-        }
-        if (phase == 2) break;
-    }
-    return ret;
-}
-
-// smem1_lds (M = false) or smem1_merged (M = true), chosen at compile time per kernel instantiation
-template <bool M, typename X, typename Z, typename Q>
-DEV int smem1_call(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S, bool &ovf,
-                   uint64_t &nblk, uint64_t &nkm)
-{
-    if constexpr (M) return smem1_merged(fm, len, q, x, min_intv, L, S, ovf, nblk, nkm);
-    else return smem1_lds(fm, len, q, x, min_intv, L, S, ovf, nblk, nkm);
-}
-
-template <typename X, typename Z, typename Q>
 DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int max_intv, Intv &mem,
-                         uint64_t &nblk, uint64_t &nkm, bool walk)
+                         uint64_t &nblk, uint64_t &nkm)
 {
     mem.x[0] = mem.x[1] = mem.x[2] = mem.info = 0;
     if (q[x] > 3) return x + 1;
@@ -771,27 +549,6 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int 
     }
     int qi = i0 < len ? q[i0] : 0;
     for (int i = i0; i < len; ++i) {
-        if (ik2 == 1 && max_intv > 1 && walk) {
-            // A unique interval stays [x0, x0] while the string follows its one occurrence (at SA[x0] in T) and
-            // is empty from the first differing base on; an empty one stays empty.  Sizes stay below max_intv, so
-            // the loop returns at the first step j >= x + min_len (or at a hole, or runs off the read): decide that
-            // step from the text instead of one bwt_extend per base.  The seed's x[1] is not tracked on this path
-            // (mem_chain reads x[0], x[2] and info only -- the same convention as the SMEM list entries).
-            const int js = i > x + min_len ? i : x + min_len;
-            const int jend = js < len ? js : len - 1;
-            int h = i;
-            while (h <= jend && q[h] < 4) ++h;
-            if (h <= jend) return h + 1;          // a hole ends the call
-            if (js >= len) return len;            // the read ends first: no seed
-            const int64_t p = fm.sa(ik0) - x, nT = fm.l_pac << 1;
-            bool match = true;
-            for (int j = i; j <= js && match; ++j) match = p + j < nT && q[j] == fm.tbase(p + j);
-            if (match) {
-                mem.x[0] = ik0; mem.x[1] = 0; mem.x[2] = 1;
-                mem.info = (uint64_t)x << 32 | (uint64_t)(js + 1);
-            }
-            return js + 1;
-        }
         const int cur = qi;
         qi = i + 1 < len ? q[i + 1] : 0;
         if (cur < 4) {
@@ -846,7 +603,7 @@ __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const 
 }
 
 // 4 waves per SIMD for u32 rows (16 one-wave blocks per CU, the LDS limit), 3 for 64-bit rows
-template <typename X, typename Z, typename Q, bool M>
+template <typename X, typename Z, typename Q>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
@@ -908,7 +665,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
         int x = 0;
         while (x < len && !ovf) {
             if (q[x] < 4) {
-                x = smem1_call<M>(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
+                x = smem1_lds(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
                 if (!ovf) take_mem1(false);
             } else ++x;
         }
@@ -917,7 +674,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
             const Intv p = S.a[k];
             const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
             if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) continue;
-            smem1_call<M>(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
+            smem1_lds(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
             if (!ovf) take_mem1(true);
         }
         if (o.max_mem_intv > 0) {
@@ -925,7 +682,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
             while (x < len && !ovf) {
                 if (q[x] < 4) {
                     Intv m;
-                    x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm, o.ss_walk != 0);
+                    x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm);
                     if (m.x[2] > 0) {
                         if (S.n >= S.cap) { ovf = true; break; }
                         Intv &d = S.a[S.n++];
@@ -958,141 +715,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
     wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
 }
 
-// k_smem_lanes: k_smem_lds with persistent lanes that step through their reads one CALL at a time.
-// In k_smem_lds a lane owns one read, and the wave runs pass 1 (bwt_smem1 over x), pass 2 (re-seeding) and pass 3
-// (bwt_seed_strategy1) as three loops: a lane whose read needs 2 bwt_smem1 calls idles while another lane of the wave
-// makes 10 (the 2 % random reads make ~10 short SMEMs), and the wave ends with its slowest read.  Here each trip of
-// the outer loop makes at most one call per lane -- one bwt_smem1 (pass 1 or 2: both lanes' kinds share the one call
-// site) or one bwt_seed_strategy1 -- after an ALU-only step that moves each lane to its next call (holes skipped,
-// pass-2 entries that do not qualify skipped, pass changes); a lane that has finished its read sorts its intervals
-// and takes the next read (li += the grid's lanes; lane = li % 64, so the wave-transposed codes and the per-wave
-// slots keep their layouts).  Per read the calls, their order and their arguments are k_smem_lds's: identical intervals.
-template <typename X, typename Z, typename Q, bool M>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lanes(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
-                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
-                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
-{
-    const int t = threadIdx.x;
-    LList<X, Z> L;   // LDS: [x0: 64*lcap X][x2: 64*lcap Z][end: 64*lcap u16]
-    L.x0 = t;
-    L.x2 = (int)((size_t)64 * lcap * sizeof(X) / sizeof(Z)) + t;
-    L.end = (int)((size_t)64 * lcap * (sizeof(X) + sizeof(Z)) / 2) + t;
-    L.stride = 64;
-    L.cap = lcap;
-    L.gcap = spill ? gcap : 0;
-    const size_t spill_tot = (size_t)(n + 63) / 64 * 64 * (size_t)gcap;
-    FM<X> fm;
-    fm.occ = ix.occ;
-    fm.occ32 = ix.occ32;
-    fm.sup = ix.sup;
-    fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2]; fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
-    fm.primary = (X)ix.primary;
-    fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
-    fm.K = ix.kmer_k;
-    fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
-    const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
-    const int lstride = gridDim.x * 64;
-    uint64_t nblk = 0, nkm = 0;
-    enum { NEXT, P1, P2, P3, FIN, DONE };
-    int st = NEXT, li = blockIdx.x * 64 + t - lstride, len = 0, x = 0, k2 = 0, old_n = 0;
-    bool ovf = false;
-    Q q{};
-    OutSlot S{SP<Intv>{intv_out}, 0, cp.intv, 0};
-    for (;;) {
-        if (st == NEXT) {   // the lane's next read
-            li += lstride;
-            if (li >= n) st = DONE;
-            else {
-                const size_t me = ((size_t)li >> 6) * 64 * (size_t)gcap + ((size_t)li & 63);
-                L.gx0 = reinterpret_cast<X *>(spill) + me;
-                L.gx2 = reinterpret_cast<Z *>(spill + spill_tot * sizeof(X)) + me;
-                L.gend = reinterpret_cast<uint32_t *>(spill + spill_tot * (sizeof(X) + sizeof(Z))) + me;
-                if constexpr (__is_same(Q, QT)) q = QT{codes + (size_t)(li >> 6) * 64 * (size_t)qcap + (li & 63)};
-                else q = codes + offs[li];
-                len = (int)(offs[li + 1] - offs[li]);
-                ovf = false;
-                S = OutSlot{SP<Intv>{intv_out + intv_slot_at_d(li, 0, cp.intv)}, 0, cp.intv, 0};
-                x = 0;
-                st = P1;
-            }
-        }
-        if (__ballot(st != DONE) == 0) break;
-        // to the lane's next call (ALU and the read's bases only)
-        int sx = 0, mi = 1;
-        bool call_smem = false, call_ss = false;
-        for (bool adv = st == P1 || st == P2 || st == P3; adv;) {
-            adv = false;
-            if (st == P1) {
-                while (x < len && q[x] > 3) ++x;
-                if (x < len && !ovf) { call_smem = true; sx = x; mi = 1; }
-                else { old_n = S.n; k2 = 0; st = P2; adv = true; }
-            } else if (st == P2) {
-                if (ovf || k2 >= old_n) { st = P3; x = 0; adv = true; }
-                else {
-                    const Intv p = S.a[k2];
-                    const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
-                    if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) { ++k2; adv = true; }
-                    else { call_smem = true; sx = (start + end) >> 1; mi = (int)p.x[2] + 1; }
-                }
-            } else if (st == P3) {
-                if (o.max_mem_intv <= 0 || ovf) st = FIN;
-                else {
-                    while (x < len && q[x] > 3) ++x;
-                    if (x < len) call_ss = true;
-                    else st = FIN;
-                }
-            }
-        }
-        if (call_smem) {   // pass 1 and pass 2 share this call site
-            const int r = smem1_call<M>(fm, len, q, sx, mi, L, S, ovf, nblk, nkm);
-            if (!ovf) {   // take_mem1
-                const bool pass2 = st == P2;
-                for (int k = 0; k < S.n1; ++k) {
-                    const Intv &m = S.a[S.cap - S.n1 + k];
-                    const uint64_t m0 = m.x[0], m2 = m.x[2], mn = m.info;
-                    const uint32_t s0 = (uint32_t)(mn >> 32), en = (uint32_t)mn;
-                    const bool keep = pass2 ? (uint64_t)(en - s0) >= (uint64_t)o.min_seed_len : (int)(en - s0) >= o.min_seed_len;
-                    if (keep) { Intv &d = S.a[S.n++]; d.x[0] = m0; d.x[1] = 0; d.x[2] = m2; d.info = mn; }
-                }
-                S.n1 = 0;
-            }
-            if (st == P1) x = r;
-            else ++k2;
-        }
-        if (call_ss) {
-            Intv m;
-            x = seed_strategy1_x<X, Z>(fm, len, q, x, o.min_seed_len, o.max_mem_intv, m, nblk, nkm, o.ss_walk != 0);
-            if (m.x[2] > 0) {
-                if (S.n >= S.cap) ovf = true;
-                else { Intv &d = S.a[S.n++]; d.x[0] = m.x[0]; d.x[1] = m.x[1]; d.x[2] = m.x[2]; d.info = m.info; }
-            }
-        }
-        if (st == FIN) {
-            if (ovf) {
-                status[li] |= ST_OVERFLOW;
-                n_intv[li] = 0;
-            } else {
-                const SP<Intv> out = S.a;
-                for (int a = 1; a < S.n; ++a) {   // equal keys are identical intervals: any correct sort is exact
-                    const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
-                    int b = a;
-                    for (; b > 0; --b) {
-                        const uint64_t pi = out[b - 1].info;
-                        if (!(ti < pi)) break;
-                        out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
-                        out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
-                    }
-                    out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
-                }
-                n_intv[li] = S.n;
-            }
-            st = NEXT;
-        }
-    }
-    wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
-    wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
-}
-
 // LDS bytes per thread for `lcap` list entries
 template <typename X, typename Z>
 static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (sizeof(X) + sizeof(Z) + 2); }
@@ -1116,620 +738,24 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int T = 64;
     int grid = (n + T - 1) / T;
     if (grid == 0) return hipSuccess;
-    // persistent lanes (k_smem_lanes, BSQ_SMEM_LANES=1; default k_smem_lds): each lane steps through rpl reads call by call
-    const char *le = getenv("BSQ_SMEM_LANES");
-    const bool lanes = le && *le == '1';
-    if (lanes) {
-        const char *r = getenv("BSQ_SMEM_RPL");
-        const int rpl = r && atoi(r) > 0 ? atoi(r) : 4;
-        grid = (grid + rpl - 1) / rpl;
-    }
     if (const char *g = getenv("BSQ_SMEM_GRID")) { const int c = atoi(g); if (c > 0 && c < grid) grid = c; }
     const int L = cp.max_len;
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
-    // the merged forward/backward loop of bwt_smem1 (smem1_merged, BSQ_SMEM_MERGE=1; default smem1_lds)
-    const char *me = getenv("BSQ_SMEM_MERGE");
-    const bool merge = me && *me == '1';
-#define BSQ_SMEM_LAUNCH2(X_, Z_, M_)                                                                                   \
-    do {                                                                                                               \
-        const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
-        if (lanes) {                                                                                                   \
-            if (codes_t)                                                                                               \
-                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, QT, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t,     \
-                                   offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                          \
-            else                                                                                                       \
-                hipLaunchKernelGGL((k_smem_lanes<X_, Z_, const uint8_t *, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, \
-                                   codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
-        } else {                                                                                                       \
-            if (codes_t)                                                                                               \
-                hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs,  \
-                                   n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                                 \
-            else                                                                                                       \
-                hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *, M_>), dim3(grid), dim3(T), sh, st, ix, o, cp,   \
-                                   codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                   \
-        }                                                                                                              \
-    } while (0)
 #define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
     do {                                                                                                               \
-        if (merge) BSQ_SMEM_LAUNCH2(X_, Z_, true);                                                                     \
-        else BSQ_SMEM_LAUNCH2(X_, Z_, false);                                                                          \
+        const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
+        if (codes_t)                                                                                                   \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,      \
+                               intv, n_intv, status, ctr, lcap, spill, gcap, L);                                       \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,    \
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                              \
     } while (0)
     if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t);
     else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
     else BSQ_SMEM_LAUNCH(uint64_t, uint64_t);
-#undef BSQ_SMEM_LAUNCH2
 #undef BSQ_SMEM_LAUNCH
-    return hipGetLastError();
-}
-
-// =============================================================================================
-// k_smem_sm: the same mem_collect_intv (bwt_smem1 x2 passes + bwt_seed_strategy1), restructured as a per-lane state
-// machine so the wave issues its memory at once (u32 rows, reads of <= SM_MAXLEN bases).
-//
-// k_smem_lds runs each lane's read as nested structured loops (forward walk, backward loop, seed strategy): a wave
-// executes a loop body only for the lanes inside it, and waits at every loop exit for its slowest lane, so its
-// rank-block loads go out with ~10 of 64 lanes active (SQ_INSTS_VMEM_RD) and the memory system sees
-// a fraction of the requests the wave could have in flight.  Here every lane is a resumable state machine:
-//   advance: each lane consumes the data its last request loaded, runs its control (divergent, ALU + LDS only)
-//            until it needs memory again, and writes up to 8 16-B load addresses into its request slots;
-//   issue:   one uniform block of 8 predicated 16-B loads for all lanes -- every lane that needs a rank block,
-//            a k-mer table row or an interval slot gets it in the same instructions.
-// A lane that finishes its read takes the next one (persistent lanes, reads li = wave + k * waves, lane = li % 64),
-// so lanes never wait for each other's reads.  The read is staged in LDS as 2-bit codes + a hole bitmap
-// (k_pack_reads), the SMEM list stays in LDS as in k_smem_lds (same LList and spill area), mem1 entries are read
-// back through the request slots (TAKE), and the final per-read sort of the intervals is k_intv_sort.  The
-// arithmetic of every step is k_smem_lds's (extend1 / ext_back2 / occ_c32 / the k-mer rows), in the same order per
-// lane, so the intervals are identical; the unique-interval text walk is not used (the extension steps it replaces
-// give the same list, one rank block per step).
-// =============================================================================================
-constexpr int SM_SLOTS = 8;
-constexpr int SM_MAXLEN = 320;   // 20 + 10 + 1 packed words <= 32 (8 slots of 16 B)
-
-enum SmState : int {
-    SMS_LOAD_REQ = 0, SMS_LOAD, SMS_P1, SMS_START, SMS_PRE, SMS_FWD_NEXT, SMS_FWD_EXT, SMS_FWD_KM, SMS_FWD_END,
-    SMS_BWD_REQ, SMS_BWD, SMS_RET, SMS_TAKE_REQ, SMS_TAKE, SMS_P2_REQ, SMS_P2, SMS_P3, SMS_SS_LOOP, SMS_SS_KM,
-    SMS_SS_NEXT, SMS_SS_EXT, SMS_FIN, SMS_DONE
-};
-
-// reads as 2-bit codes (code & 3, 16 per word, base i at bits 2(i & 15) of word i >> 4), then a hole bitmap (code > 3,
-// 32 per word), then the length; nwp words per read (a multiple of 4: whole 16-B slots)
-__global__ void __launch_bounds__(256) k_pack_reads(const uint8_t *codes, const int64_t *offs, int n, int nwp, int nw2,
-                                                    int nwh, uint32_t *qpack)
-{
-    const int li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= n) return;
-    const uint8_t *q = codes + offs[li];
-    const int len = (int)(offs[li + 1] - offs[li]);
-    uint32_t *o = qpack + (size_t)li * nwp;
-    for (int w = 0; w < nw2; ++w) {
-        uint32_t v = 0;
-        for (int t = 0; t < 16; ++t) { const int i = w * 16 + t; if (i < len) v |= (uint32_t)(q[i] & 3) << (2 * t); }
-        o[w] = v;
-    }
-    for (int w = 0; w < nwh; ++w) {
-        uint32_t v = 0;
-        for (int t = 0; t < 32; ++t) { const int i = w * 32 + t; if (i < len && q[i] > 3) v |= 1u << t; }
-        o[nw2 + w] = v;
-    }
-    o[nw2 + nwh] = (uint32_t)len;
-    for (int w = nw2 + nwh + 1; w < nwp; ++w) o[w] = 0;
-}
-
-// the per-read interval sort that ends k_smem_lds (mem_collect_intv's ks_introsort by info: equal keys are identical
-// intervals, so any correct sort is exact), one lane per read over its wave-interleaved slots
-__global__ void __launch_bounds__(256) k_intv_sort(int n, Intv *intv_out, const int32_t *n_intv, int cap)
-{
-    const int li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= n) return;
-    const int m = n_intv[li];
-    const SP<Intv> out{intv_out + intv_slot_at_d(li, 0, cap)};
-    for (int a = 1; a < m; ++a) {
-        const uint64_t t0 = out[a].x[0], t1 = out[a].x[1], t2 = out[a].x[2], ti = out[a].info;
-        int b = a;
-        for (; b > 0; --b) {
-            const uint64_t pi = out[b - 1].info;
-            if (!(ti < pi)) break;
-            out[b].x[0] = out[b - 1].x[0]; out[b].x[1] = out[b - 1].x[1];
-            out[b].x[2] = out[b - 1].x[2]; out[b].info = pi;
-        }
-        out[b].x[0] = t0; out[b].x[1] = t1; out[b].x[2] = t2; out[b].info = ti;
-    }
-}
-
-// rank sums of base c at both ends of the interval [a - 1, a - 1 + x2] from the blocks loaded into slots s0..s0+3
-// (k end: s0, s0+1; l end: s0+2, s0+3, or the k end's block again when both ends share it)
-template <int S0>
-DEV void sm_sums(const FM<uint32_t> &fm, const uint4 (&D)[SM_SLOTS], uint32_t a, uint32_t x2, int c, uint32_t &kc,
-                 uint32_t &kg, uint32_t &lc, uint32_t &lg, uint64_t &nblk)
-{
-    const uint32_t k = a - 1, l = k + x2;
-    const bool knone = k == 0xffffffffu;
-    const uint32_t kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-    const bool same = !knone && (kk >> 6) == (ll >> 6);
-    const uint4 wk[2] = {D[S0], D[S0 + 1]};
-    const uint4 wl[2] = {same ? D[S0] : D[S0 + 2], same ? D[S0 + 1] : D[S0 + 3]};
-    occ_c32(wk, kk, knone, c, kc, kg);
-    occ_c32(wl, ll, false, c, lc, lg);
-    nblk += (knone || same) ? 1 : 2;
-}
-
-// the request for sm_sums<S0>: the k end's block unless k = -1, the l end's unless it is the same block
-template <int S0>
-DEV void sm_req_blocks(const FM<uint32_t> &fm, uint32_t a, uint32_t x2, const uint4 *(&ad)[SM_SLOTS], uint32_t &vm)
-{
-    const uint32_t k = a - 1, l = k + x2;
-    const bool knone = k == 0xffffffffu;
-    const uint32_t kk = k - (k >= fm.primary), ll = l - (l >= fm.primary);
-    if (!knone) { ad[S0] = reinterpret_cast<const uint4 *>(fm.occ32 + (kk >> 6)); ad[S0 + 1] = ad[S0] + 1; vm |= 3u << S0; }
-    if (knone || (kk >> 6) != (ll >> 6)) {
-        ad[S0 + 2] = reinterpret_cast<const uint4 *>(fm.occ32 + (ll >> 6)); ad[S0 + 3] = ad[S0 + 2] + 1; vm |= 12u << S0;
-    }
-}
-
-DEV uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)hi << 32 | lo; }
-
-__global__ void __launch_bounds__(64) k_smem_sm(DIndex ix, DOpts o, Caps cp, const uint32_t *qpack, int nwp, int nw2,
-                                                int nwh, int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
-                                                Counters *ctr, int lcap, uint8_t *spill, int gcap)
-{
-    const int lane = threadIdx.x;
-    FM<uint32_t> fm;
-    fm.occ = ix.occ;
-    fm.occ32 = ix.occ32;
-    fm.sup = ix.sup;
-    fm.l2_0 = (uint32_t)ix.L2[0]; fm.l2_1 = (uint32_t)ix.L2[1]; fm.l2_2 = (uint32_t)ix.L2[2];
-    fm.l2_3 = (uint32_t)ix.L2[3]; fm.l2_4 = (uint32_t)ix.L2[4];
-    fm.primary = (uint32_t)ix.primary;
-    fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
-    fm.K = ix.kmer_k < 11 ? ix.kmer_k : 11;   // this kernel uses levels <= 11 of a deeper table
-    fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
-    const int K = fm.K;
-    // LDS (u32 units): the read's nwp words lane-interleaved, then the list [x0: 64*lcap][x2: 64*lcap][end: 64*lcap u16]
-    LList<uint32_t, uint32_t> L;
-    const int lbase = nwp * 64;
-    L.x0 = lbase + lane;
-    L.x2 = lbase + 64 * lcap + lane;
-    L.end = 2 * (lbase + 128 * lcap) + lane;
-    L.stride = 64;
-    L.cap = lcap;
-    L.gcap = spill ? gcap : 0;
-    const size_t spill_tot = (size_t)(n + 63) / 64 * 64 * (size_t)gcap;
-    auto qw = [&](int w) -> uint32_t { return g_smem_u32[w * 64 + lane]; };
-    auto q2 = [&](int i) -> int { return (int)(qw(i >> 4) >> ((i & 15) << 1) & 3u); };
-    auto qv = [&](int i) -> int { return (qw(nw2 + (i >> 5)) >> (i & 31) & 1u) ? 4 : q2(i); };
-    const int split_len = (int)(o.min_seed_len * o.split_factor + .499);
-    const int cap = cp.intv;
-
-    uint64_t nblk = 0, nkm = 0;
-    int st = SMS_LOAD_REQ;
-    int li = blockIdx.x * 64 + lane;
-    const int lstride = gridDim.x * 64;
-    SP<Intv> Sa{nullptr};
-    int len = 0, Sn = 0, Sn1 = 0, x = 0, k2 = 0, old_n = 0, ret_to = 0, tk = 0;
-    bool ovf = false;
-    // bwt_smem1 / bwt_seed_strategy1 state
-    int sx = 0, min_intv = 1, ikend = 0, n_l = 0, i = 0, nt = 0, Lt = 0, pt = 0, ret = 0, last_start = 0, c = 0, nc = 0,
-        j = 0;
-    uint32_t ik0 = 0, ik1 = 0, ik2 = 0, fcode = 0, wcode = 0, last_x2 = 0;
-    bool stop = false, ta = false, tb = false, hb = false, kmreq = false;
-    uint32_t pa0 = 0, pa2 = 0, pb0 = 0, pb2 = 0;
-    int pae = 0, pbe = 0;
-    uint4 D[SM_SLOTS];
-#pragma unroll
-    for (int s = 0; s < SM_SLOTS; ++s) D[s] = make_uint4(0, 0, 0, 0);
-    // termination guard: no read needs 2^20 trips (a 320-base read takes a few thousand); should a lane ever cycle,
-    // the wave stops and hands every read it still owns to the retry pass instead of spinning on the device
-    const int64_t trip_cap = (int64_t)((n - 1 - (int)blockIdx.x * 64) / lstride + 1) << 20;
-    int64_t trips = 0;
-    bool stuck = false;
-
-    for (;;) {
-        const uint4 *ad[SM_SLOTS];
-        uint32_t vm = 0;
-        int spins = 0;
-        for (bool go = true; go;) {
-            if (++spins > (1 << 16)) { stuck = true; break; }
-            switch (st) {
-            case SMS_LOAD_REQ: {
-                if (li >= n) { st = SMS_DONE; go = false; break; }
-                const uint4 *p = reinterpret_cast<const uint4 *>(qpack + (size_t)li * nwp);
-#pragma unroll
-                for (int s = 0; s < SM_SLOTS; ++s)
-                    if (4 * s < nwp) { ad[s] = p + s; vm |= 1u << s; }
-                st = SMS_LOAD; go = false;
-                break;
-            }
-            case SMS_LOAD: {
-#pragma unroll
-                for (int s = 0; s < SM_SLOTS; ++s)
-                    if (4 * s < nwp) {
-                        g_smem_u32[(4 * s) * 64 + lane] = D[s].x; g_smem_u32[(4 * s + 1) * 64 + lane] = D[s].y;
-                        g_smem_u32[(4 * s + 2) * 64 + lane] = D[s].z; g_smem_u32[(4 * s + 3) * 64 + lane] = D[s].w;
-                    }
-                len = (int)qw(nw2 + nwh);
-                Sa = SP<Intv>{intv_out + intv_slot_at_d(li, 0, cap)};
-                {
-                    const size_t me = ((size_t)li >> 6) * 64 * (size_t)gcap + ((size_t)li & 63);
-                    L.gx0 = reinterpret_cast<uint32_t *>(spill) + me;
-                    L.gx2 = reinterpret_cast<uint32_t *>(spill + spill_tot * 4) + me;
-                    L.gend = reinterpret_cast<uint32_t *>(spill + spill_tot * 8) + me;
-                }
-                Sn = 0; Sn1 = 0; ovf = false; x = 0;
-                st = SMS_P1;
-                break;
-            }
-            case SMS_P1: {   // while (x < len) { if (q[x] < 4) x = smem1(x, 1), take_mem1; else ++x; }
-                while (x < len && qv(x) > 3) ++x;
-                if (x >= len) { old_n = Sn; k2 = 0; st = SMS_P2_REQ; break; }
-                sx = x; min_intv = 1; ret_to = 0;
-                st = SMS_START;
-                break;
-            }
-            case SMS_START: {   // bwt_smem1 entry and its forward k-mer prefix (smem1_lds lines 316-347)
-                Sn1 = 0;
-                const int c0 = qv(sx);
-                if (c0 > 3) { ret = sx + 1; st = SMS_RET; break; }
-                if (min_intv < 1) min_intv = 1;
-                ik0 = fm.L2(c0) + 1; ik1 = fm.L2(3 - c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0);
-                ikend = sx + 1; n_l = 0; i = sx + 1; fcode = (uint32_t)c0; stop = false;
-                Lt = K < len - sx ? K : len - sx;
-                nt = 1;
-                while (nt < Lt && qv(sx + nt) < 4) ++nt;
-                pt = 2;
-                if (nt >= 2) {
-#pragma unroll
-                    for (int s = 0; s < SM_SLOTS; ++s) {
-                        const int t = pt + s;
-                        if (t <= nt) {
-                            fcode = fcode << 2 | (uint32_t)q2(sx + t - 1);
-                            ad[s] = fm.kt + koff(t) + fcode; vm |= 1u << s;
-                        }
-                    }
-                    st = SMS_PRE; go = false;
-                    break;
-                }
-                // no prefix rows: the post-prefix bookkeeping below
-                if (!stop) {
-                    i = sx + nt;
-                    if (nt < Lt) {
-                        if (n_l >= L.total()) { ovf = true; st = SMS_FIN; break; }
-                        L.set(n_l++, ik0, ik2, ikend);
-                        stop = true;
-                    }
-                }
-                st = stop ? SMS_FWD_END : SMS_FWD_NEXT;
-                break;
-            }
-            case SMS_PRE: {   // consume prefix rows pt .. min(nt, pt + 7)
-                const int last = nt < pt + SM_SLOTS - 1 ? nt : pt + SM_SLOTS - 1;
-                nkm += (uint64_t)(last - pt + 1);
-#pragma unroll
-                for (int s = 0; s < SM_SLOTS; ++s) {
-                    const int t = pt + s;
-                    if (t <= last && !stop && !ovf) {
-                        const uint32_t n0 = D[s].x, n2 = D[s].y;
-                        if (n2 != ik2) {
-                            if (n_l >= L.total()) ovf = true;
-                            else {
-                                L.set(n_l++, ik0, ik2, ikend);
-                                if (n2 < (uint32_t)min_intv) { stop = true; i = sx + t - 1; }
-                            }
-                        }
-                        if (!stop && !ovf) { ik0 = n0; ik2 = n2; ikend = sx + t; }
-                    }
-                }
-                if (ovf) { st = SMS_FIN; break; }
-                if (!stop && last == nt) {
-#pragma unroll
-                    for (int s = 0; s < SM_SLOTS; ++s) if (s == nt - pt) ik1 = D[s].z;   // x[1] of row nt
-                }
-                pt = last + 1;
-                if (!stop && pt <= nt) {   // the next rows
-#pragma unroll
-                    for (int s = 0; s < SM_SLOTS; ++s) {
-                        const int t = pt + s;
-                        if (t <= nt) {
-                            fcode = fcode << 2 | (uint32_t)q2(sx + t - 1);
-                            ad[s] = fm.kt + koff(t) + fcode; vm |= 1u << s;
-                        }
-                    }
-                    go = false;
-                    break;
-                }
-                if (!stop) {
-                    i = sx + nt;
-                    if (nt < Lt) {
-                        if (n_l >= L.total()) { ovf = true; st = SMS_FIN; break; }
-                        L.set(n_l++, ik0, ik2, ikend);
-                        stop = true;
-                    }
-                }
-                st = stop ? SMS_FWD_END : SMS_FWD_NEXT;
-                break;
-            }
-            case SMS_FWD_NEXT: {   // one forward extension (smem1_lds lines 376-430, without the text walk)
-                if (stop || i >= len) { st = SMS_FWD_END; break; }
-                const int cur = qv(i);
-                if (cur < 4) {
-                    c = 3 - cur;
-                    fcode = fcode << 2 | (uint32_t)cur;
-                    if (i - sx + 1 <= K) { ad[0] = fm.kt + koff(i - sx + 1) + fcode; vm |= 1u; st = SMS_FWD_KM; }
-                    else { sm_req_blocks<0>(fm, ik1, ik2, ad, vm); st = SMS_FWD_EXT; }
-                    go = false;
-                } else {
-                    if (n_l >= L.total()) { ovf = true; st = SMS_FIN; break; }
-                    L.set(n_l++, ik0, ik2, ikend);
-                    st = SMS_FWD_END;
-                }
-                break;
-            }
-            case SMS_FWD_EXT:
-            case SMS_FWD_KM: {
-                uint32_t n0, n1, n2;
-                if (st == SMS_FWD_KM) { n0 = D[0].x; n2 = D[0].y; n1 = D[0].z; ++nkm; }
-                else {   // extend1(fm, ik1, ik0, ik2, c): a = ik1, o = ik0
-                    uint32_t kc, kg, lc, lg;
-                    sm_sums<0>(fm, D, ik1, ik2, c, kc, kg, lc, lg, nblk);
-                    n1 = fm.L2(c) + 1 + kc;
-                    n2 = lc - kc;
-                    n0 = ik0 + (uint32_t)(ik1 <= fm.primary && ik1 + ik2 - 1 >= fm.primary) + (lg - kg);
-                }
-                if (n2 != ik2) {
-                    if (n_l >= L.total()) { ovf = true; st = SMS_FIN; break; }
-                    L.set(n_l++, ik0, ik2, ikend);
-                    if (n2 < (uint32_t)min_intv) { st = SMS_FWD_END; break; }
-                }
-                ik0 = n0; ik1 = n1; ik2 = n2; ikend = i + 1; ++i;
-                st = SMS_FWD_NEXT;
-                break;
-            }
-            case SMS_FWD_END: {   // final push, reversal, backward-loop setup (smem1_lds lines 431-457)
-                if (i == len) {
-                    if (n_l >= L.total()) { ovf = true; st = SMS_FIN; break; }
-                    L.set(n_l++, ik0, ik2, ikend);
-                }
-                for (int jj = 0; jj < (n_l >> 1); ++jj) {
-                    uint32_t a0, b0, a2, b2;
-                    int ae, be;
-                    L.get(jj, a0, a2, ae);
-                    L.get(n_l - 1 - jj, b0, b2, be);
-                    L.set(jj, b0, b2, be);
-                    L.set(n_l - 1 - jj, a0, a2, ae);
-                }
-                { uint32_t d0, d2; L.get(0, d0, d2, ret); }
-                last_start = 0x7fffffff;
-                wcode = 0;
-                for (int t = 0; t < K; ++t) wcode = wcode << 2 | (sx + t < len ? (uint32_t)q2(sx + t) : 0u);
-                i = sx - 1;
-                c = i < 0 ? -1 : (qv(i) < 4 ? qv(i) : -1);
-                if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
-                nc = 0; j = 0; last_x2 = 0;
-                st = SMS_BWD_REQ;
-                break;
-            }
-            case SMS_BWD_REQ: {   // entries j, j+1 of position i: their k-mer rows or rank blocks
-                hb = j + 1 < n_l;
-                L.get(j, pa0, pa2, pae);
-                L.get(hb ? j + 1 : j, pb0, pb2, pbe);
-                if (c >= 0) {
-                    const int La = pae - i, Lb = pbe - i;
-                    ta = La <= K; tb = hb && Lb <= K;
-                    if (ta) { ad[0] = fm.kt + koff(La) + (wcode >> (2 * (K - La))); vm |= 1u; }
-                    else sm_req_blocks<0>(fm, pa0, pa2, ad, vm);
-                    if (hb) {
-                        if (tb) { ad[4] = fm.kt + koff(Lb) + (wcode >> (2 * (K - Lb))); vm |= 16u; }
-                        else sm_req_blocks<4>(fm, pb0, pb2, ad, vm);
-                    }
-                    st = SMS_BWD; go = false;
-                } else st = SMS_BWD;
-                break;
-            }
-            case SMS_BWD: {   // smem1_lds lines 470-511
-                uint32_t oa0 = 0, ob0 = 0, oa2 = 0, ob2 = 0;
-                if (c >= 0) {
-                    uint32_t kc, kg, lc, lg;
-                    if (ta) { oa0 = D[0].x; oa2 = D[0].y; }
-                    else { sm_sums<0>(fm, D, pa0, pa2, c, kc, kg, lc, lg, nblk); oa0 = fm.L2(c) + 1 + kc; oa2 = lc - kc; }
-                    if (hb) {
-                        if (tb) { ob0 = D[4].x; ob2 = D[4].y; }
-                        else { sm_sums<4>(fm, D, pb0, pb2, c, kc, kg, lc, lg, nblk); ob0 = fm.L2(c) + 1 + kc; ob2 = lc - kc; }
-                    }
-                    nkm += (uint64_t)ta + (uint64_t)(hb && tb);
-                }
-                for (int h = 0; h < 2; ++h) {
-                    if (h == 1 && !hb) break;
-                    const uint32_t p0 = h ? pb0 : pa0, o0 = h ? ob0 : oa0, p2 = h ? pb2 : pa2, o2 = h ? ob2 : oa2;
-                    const int pe = h ? pbe : pae;
-                    const bool keep_hit = c < 0 || o2 < (uint32_t)min_intv;
-                    if (keep_hit) {
-                        if (nc == 0 && (Sn1 == 0 || i + 1 < last_start)) {
-                            if (Sn + Sn1 >= cap) { ovf = true; break; }
-                            Intv &m = Sa[cap - 1 - Sn1];
-                            m.x[0] = p0; m.x[1] = 0; m.x[2] = p2;
-                            m.info = (uint64_t)(uint32_t)(i + 1) << 32 | (uint32_t)pe;
-                            ++Sn1;
-                            last_start = i + 1;
-                        }
-                    } else if (nc == 0 || o2 != last_x2) {
-                        L.set(nc++, o0, o2, pe);
-                        last_x2 = o2;
-                    }
-                }
-                if (ovf) { st = SMS_FIN; break; }
-                j += 2;
-                st = SMS_BWD_REQ;
-                if (j >= n_l) {
-                    if (nc == 0) { st = SMS_RET; break; }
-                    n_l = nc; nc = 0; j = 0; last_x2 = 0;
-                    --i;
-                    c = i < 0 ? -1 : (qv(i) < 4 ? qv(i) : -1);
-                    if (K > 0 && c >= 0) wcode = wcode >> 2 | (uint32_t)c << (2 * (K - 1));
-                }
-                break;
-            }
-            case SMS_RET: {   // back in the caller: pass 1 continues at x = ret; both passes take mem1 first
-                if (ret_to == 0) x = ret;
-                tk = 0;
-                st = SMS_TAKE_REQ;
-                break;
-            }
-            case SMS_TAKE_REQ: {   // take_mem1: mem1 (reversed emission order) sits at Sa[cap - Sn1 .. cap)
-                if (tk >= Sn1) {
-                    Sn1 = 0;
-                    if (ret_to == 0) st = SMS_P1;
-                    else { ++k2; st = SMS_P2_REQ; }
-                    break;
-                }
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    if (tk + s < Sn1) {
-                        const uint4 *e = reinterpret_cast<const uint4 *>(&Sa[cap - Sn1 + tk + s]);
-                        ad[2 * s] = e; ad[2 * s + 1] = e + 1; vm |= 3u << (2 * s);
-                    }
-                st = SMS_TAKE; go = false;
-                break;
-            }
-            case SMS_TAKE: {
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    if (tk + s < Sn1) {
-                        const uint64_t m0 = u64_of(D[2 * s].x, D[2 * s].y), m2 = u64_of(D[2 * s + 1].x, D[2 * s + 1].y);
-                        const uint64_t mi = u64_of(D[2 * s + 1].z, D[2 * s + 1].w);
-                        const uint32_t s0 = (uint32_t)(mi >> 32), en = (uint32_t)mi;
-                        const bool keep = ret_to ? (uint64_t)(en - s0) >= (uint64_t)o.min_seed_len : (int)(en - s0) >= o.min_seed_len;
-                        if (keep) { Intv &d = Sa[Sn++]; d.x[0] = m0; d.x[1] = 0; d.x[2] = m2; d.info = mi; }
-                    }
-                tk += 4;
-                st = SMS_TAKE_REQ;
-                break;
-            }
-            case SMS_P2_REQ: {   // pass 2: re-seed long SMEMs of few occurrences from their middle
-                if (k2 >= old_n) { st = SMS_P3; break; }
-                const uint4 *e = reinterpret_cast<const uint4 *>(&Sa[k2]);
-                ad[0] = e; ad[1] = e + 1; vm |= 3u;
-                st = SMS_P2; go = false;
-                break;
-            }
-            case SMS_P2: {
-                const uint64_t px2 = u64_of(D[1].x, D[1].y), pinfo = u64_of(D[1].z, D[1].w);
-                const int start = (int)(pinfo >> 32), end = (int)(uint32_t)pinfo;
-                if (end - start < split_len || px2 > (uint64_t)o.split_width) { ++k2; st = SMS_P2_REQ; break; }
-                sx = (start + end) >> 1; min_intv = (int)px2 + 1; ret_to = 1;
-                st = SMS_START;
-                break;
-            }
-            case SMS_P3: {
-                if (o.max_mem_intv > 0) { x = 0; st = SMS_SS_LOOP; } else st = SMS_FIN;
-                break;
-            }
-            case SMS_SS_LOOP: {   // bwt_seed_strategy1 over x (seed_strategy1_x)
-                while (x < len && qv(x) > 3) ++x;
-                if (x >= len) { st = SMS_FIN; break; }
-                const int c0 = qv(x);
-                ik0 = fm.L2(c0) + 1; ik1 = fm.L2(3 - c0) + 1; ik2 = fm.L2(c0 + 1) - fm.L2(c0);
-                fcode = (uint32_t)c0;
-                i = x + 1;
-                st = SMS_SS_NEXT;
-                if (K > 1 && o.min_seed_len >= K) {
-                    const int Ls = K < len - x ? K : len - x;
-                    int t = 1;
-                    for (; t < Ls; ++t) {
-                        const int cc = qv(x + t);
-                        if (cc > 3) break;
-                        fcode = fcode << 2 | (uint32_t)cc;
-                    }
-                    if (t < Ls) { x = x + t + 1; st = SMS_SS_LOOP; break; }
-                    i = x + Ls;
-                    if (Ls > 1) { ad[0] = fm.kt + koff(Ls) + fcode; vm |= 1u; st = SMS_SS_KM; go = false; }
-                }
-                break;
-            }
-            case SMS_SS_KM: {
-                ik0 = D[0].x; ik2 = D[0].y; ik1 = D[0].z; ++nkm;
-                st = SMS_SS_NEXT;
-                break;
-            }
-            case SMS_SS_NEXT: {
-                if (i >= len) { x = len; st = SMS_SS_LOOP; break; }
-                const int cur = qv(i);
-                if (cur > 3) { x = i + 1; st = SMS_SS_LOOP; break; }
-                c = 3 - cur;
-                fcode = fcode << 2 | (uint32_t)cur;
-                kmreq = i - x + 1 <= K;
-                if (kmreq) { ad[0] = fm.kt + koff(i - x + 1) + fcode; vm |= 1u; }
-                else sm_req_blocks<0>(fm, ik1, ik2, ad, vm);
-                st = SMS_SS_EXT; go = false;
-                break;
-            }
-            case SMS_SS_EXT: {
-                uint32_t n0, n1, n2;
-                if (kmreq) { n0 = D[0].x; n2 = D[0].y; n1 = D[0].z; ++nkm; }
-                else {
-                    uint32_t kc, kg, lc, lg;
-                    sm_sums<0>(fm, D, ik1, ik2, c, kc, kg, lc, lg, nblk);
-                    n1 = fm.L2(c) + 1 + kc;
-                    n2 = lc - kc;
-                    n0 = ik0 + (uint32_t)(ik1 <= fm.primary && ik1 + ik2 - 1 >= fm.primary) + (lg - kg);
-                }
-                if (n2 < (uint32_t)o.max_mem_intv && i - x >= o.min_seed_len) {
-                    if (n2 > 0) {
-                        if (Sn >= cap) { ovf = true; st = SMS_FIN; break; }
-                        Intv &d = Sa[Sn++];
-                        d.x[0] = n0; d.x[1] = n1; d.x[2] = n2; d.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
-                    }
-                    x = i + 1;
-                    st = SMS_SS_LOOP;
-                } else {
-                    ik0 = n0; ik1 = n1; ik2 = n2; ++i;
-                    st = SMS_SS_NEXT;
-                }
-                break;
-            }
-            case SMS_FIN: {
-                if (ovf) { atomicOr(&status[li], ST_OVERFLOW); n_intv[li] = 0; }
-                else n_intv[li] = Sn;
-                li += lstride;
-                st = SMS_LOAD_REQ;
-                break;
-            }
-            default:   // SMS_DONE
-                go = false;
-                break;
-            }
-        }
-        if (__ballot(stuck) != 0 || ++trips > trip_cap) {
-            for (; li < n; li += lstride) { atomicOr(&status[li], ST_OVERFLOW); n_intv[li] = 0; }
-            break;
-        }
-        if (__ballot(st != SMS_DONE) == 0) break;
-#pragma unroll
-        for (int s = 0; s < SM_SLOTS; ++s)
-            if (vm & (1u << s)) D[s] = *ad[s];
-    }
-    wave_add2(&ctr[STG_SMEM].occ_blocks, nblk);
-    wave_add2(&ctr[STG_SMEM].kmer_hits, nkm);
-}
-
-// Main-pass seeding through k_smem_sm (u32 rows, max_len <= SM_MAXLEN): pack the reads, run the lanes, sort the
-// intervals of each read.  qpack: a workspace buffer of n * sm_words(max_len) u32.
-int sm_words(int max_len) { return ((max_len + 15) / 16 + (max_len + 31) / 32 + 1 + 3) & ~3; }
-bool sm_applies(const DIndex &ix, int max_len) { return !ix.wide && max_len <= SM_MAXLEN; }
-
-hipError_t launch_smem_sm(hipStream_t st, const DIndex &ix, const DOpts &o, const Caps &cp, const uint8_t *codes,
-                          const int64_t *offs, int n, Intv *intv, int32_t *n_intv, uint32_t *status, Counters *ctr,
-                          int lcap, uint8_t *spill, int gcap, uint32_t *qpack, int reads_per_lane)
-{
-    if (n <= 0) return hipSuccess;
-    const int nw2 = (cp.max_len + 15) / 16, nwh = (cp.max_len + 31) / 32, nwp = sm_words(cp.max_len);
-    hipLaunchKernelGGL(k_pack_reads, dim3((n + 255) / 256), dim3(256), 0, st, codes, offs, n, nwp, nw2, nwh, qpack);
-    const int waves = (n + 63) / 64;
-    const int rpl = reads_per_lane > 0 ? reads_per_lane : 1;
-    const int grid = (waves + rpl - 1) / rpl;
-    const size_t sh = (size_t)nwp * 64 * 4 + lds_bytes<uint32_t, uint32_t>(64, lcap);
-    hipLaunchKernelGGL(k_smem_sm, dim3(grid), dim3(64), sh, st, ix, o, cp, (const uint32_t *)qpack, nwp, nw2, nwh, n, intv,
-                       n_intv, status, ctr, lcap, spill, gcap);
-    hipLaunchKernelGGL(k_intv_sort, dim3((n + 255) / 256), dim3(256), 0, st, n, intv, (const int32_t *)n_intv, cp.intv);
     return hipGetLastError();
 }
 
