@@ -322,15 +322,17 @@ struct IndexMeta {   // fixed header of the metadata blob; followed by Ann[n_ann
     uint64_t table_bytes[T_N];
 };
 
-static int kmer_depth(uint64_t seq_len)
+static int kmer_depth(uint64_t seq_len, bool wide)
 {
     if (seq_len == 0) return 0;
     // ~log4(rows), at most 10 while the rank blocks (32 B per 64 rows) fit the 256 MB Infinity Cache: the table
     // competes with them for it (C3, 100 MB of rank blocks: seeding 10.45 ms at K = 10 with a 22 MB table, 10.7 at
     // 11 with 89 MB, 11.3-12.1 at 12-14, 10.9 at 9); else at most 13: the rank blocks' lines miss anyway and each
     // level answers more backward extensions with one line (C4, 3 Gbp: 28.0 M reads/s at 11, 30.0 M at 13 with a
-    // 2.9 GB table)
-    const int kmax = seq_len / 2 > (256ull << 20) ? 13 : 10;
+    // 2.9 GB table).  Depth 13 only for 64-bit rows, the kernels that preload 13 levels
+    // (and the only ones measured there): u32 rows of a 256 Mbp - 2 Gbp text stay at 10, where u32 kernels preload
+    // 11 levels and read deeper ones one per step (slower at C3: 11.3-12.1 ms against 10.45).
+    const int kmax = wide && seq_len / 2 > (256ull << 20) ? 13 : 10;
     int K = 0;
     while (K < kmax && (1ull << (2 * (K + 1))) <= seq_len) ++K;
     // BSQ_KMER_K: 0 disables; up to 15 (the kernels preload levels <= 11 and read deeper levels one per step;
@@ -353,7 +355,7 @@ static void table_sizes(const HostIndex &h, uint64_t bytes[T_N], int &K, int &wi
     bytes[T_OCC32] = nblk * 2 * sizeof(OccBlock32) + (wide ? occ32_sup_count(2 * nblk) * sizeof(SupBlock) : 0);
     bytes[T_SA] = (h.seq_len + 1) * (wide ? 8 : 4);
     bytes[T_PAC] = h.pac.size() + 16;
-    K = kmer_depth(h.seq_len);
+    K = kmer_depth(h.seq_len, wide != 0);
     bytes[T_KMER] = K ? (((uint64_t)1 << (2 * (K + 1))) - 4) / 3 * (wide ? 32 : 16) : 0;
 }
 

@@ -126,6 +126,23 @@ class RcclTransport final : public bsq::xchg::Transport {
         }
     }
 
+    // the exchange thread waiting for a lane to publish: RCCL's asynchronous error, and the same deadline as sync_xs
+    // (a lane whose stream waits on an unmatched send blocks in its next HIP call; abort() then releases it)
+    int poll(double waited_s, std::string &err) override
+    {
+        ncclResult_t async = ncclSuccess;
+        if (comm && ncclCommGetAsyncError(comm, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress) {
+            err = std::string("RCCL: ") + ncclGetErrorString(async);
+            return BSQ_E_HIP;
+        }
+        if (waited_s > timeout_s) {
+            err = "timed out after " + std::to_string((int)timeout_s) +
+                  " s waiting for a local batch (its stream may wait on a send no other rank matched; BSQ_XCHG_TIMEOUT_S)";
+            return BSQ_E_HIP;
+        }
+        return BSQ_OK;
+    }
+
     int all_gather(int, const int64_t mine[4], int64_t *all, std::string &err) override
     {
         THIP(hipSetDevice(device_));

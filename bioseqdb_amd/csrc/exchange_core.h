@@ -75,7 +75,13 @@ class Transport {
     virtual int recv(int lane, const std::vector<Parts> &parts, const std::vector<int64_t> &at, int64_t total,
                      std::string &err) = 0;
     // batch thread, before its lane's next round: order the batch's next writes after the lane's last send
+    // (RCCL: a device-side wait -- the batch's next blocking HIP call can then wait on that send indefinitely)
     virtual int batch_resume(int lane, std::string &err) = 0;
+    // exchange thread, while it has waited `waited_s` for a lane to publish its next round: nonzero (with `err`)
+    // ends the wait as a failure -- a transport error, or a deadline.  A lane blocked behind a send that no peer
+    // will ever match (rank 0 died, or its receive failed locally) publishes nothing, so without this the exchange
+    // thread would wait forever; the failure aborts the transport, which releases the blocked device waits.
+    virtual int poll(double waited_s, std::string &err) { (void)waited_s; (void)err; return 0; }
     // every rank stops (a failure reported by some rank, or this rank's transport error)
     virtual void abort() {}
 };
@@ -148,16 +154,28 @@ class Core {
         for (int k = 0; k < rounds && !rc; ++k) {
             for (int i = 0; i < L && !rc; ++i) {
                 Records rec;
-                int st;
+                int st = 0;
+                std::string e;
                 {
                     std::unique_lock<std::mutex> lk(mu);
                     Pub &p = pub[(size_t)i];
-                    cv.wait(lk, [&] { return p.round >= k; });
+                    const auto t0 = std::chrono::steady_clock::now();
+                    while (!cv.wait_for(lk, std::chrono::milliseconds(5), [&] { return p.round >= k; })) {
+                        lk.unlock();
+                        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                        const int prc = t_.poll(waited, e);
+                        lk.lock();
+                        if (prc) { if (e.empty()) e = "transport poll failed"; break; }
+                    }
+                    if (!e.empty()) {
+                        rc = fail(-3, "exchange (round " + std::to_string(k) + ", lane " + std::to_string(i) +
+                                  ") waiting for the lane's batch: " + e, first);
+                        break;
+                    }
                     rec = p.rec;
                     st = p.status;
                 }
                 const int64_t mine[4] = {st ? 0 : rec.n_reads, st ? 0 : rec.n_hits, st ? 0 : rec.n_cigar, (int64_t)st};
-                std::string e;
                 if (t_.all_gather(i, mine, all.data(), e)) {
                     rc = fail(-3, "exchange all-gather (round " + std::to_string(k) + ", lane " + std::to_string(i) + "): " + e, first);
                     break;

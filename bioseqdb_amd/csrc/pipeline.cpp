@@ -198,8 +198,12 @@ int align_job(bsq_pipeline *p, Slot &x)
     const std::string err = rc ? std::string(bsq_last_error()) : std::string();
     ws = batch_detach_workspaces(x.batch);
     if (ws) {
-        std::lock_guard<std::mutex> lk(p->mu);
-        p->pool.push_back(ws);
+        // at most run_cap sets are kept: a batch that brought its own set (a group re-run) would otherwise grow the
+        // pool past the alignments that can use it at once (~8.5 GB each)
+        std::unique_lock<std::mutex> lk(p->mu);
+        if ((int)p->pool.size() < p->run_cap) { p->pool.push_back(ws); ws = nullptr; }
+        lk.unlock();
+        workspaces_free(ws);
     }
     if (rc) { set_error(err); return rc; }
     x.t[3] = now_ms();

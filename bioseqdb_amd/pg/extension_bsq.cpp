@@ -138,11 +138,13 @@ constexpr long kRefFetchRows = 64;   // reference rows are long; their bytes are
 
 // iterate_nuclseq_table (extension.cpp:156-195): (int2/4/8 id, nuclseq) rows of `sql`, NULL rows skipped,
 // the column types checked on every fetch with the reference's messages.  Each fetch of up to `fetch` rows is
-// handed to on_rows(ids, seqs) while its tuples are valid, then released.
-// If on_rows returns a ticket >= 0 (a deferred pipeline submission that still reads the tuples), the tuples of that
-// fetch are freed only after the NEXT fetch has been fetched and handed over and wait(ticket) has returned, so the
-// staging of fetch k runs on a pipeline worker while this backend fetches k+1.  Unwinding with a ticket
-// outstanding waits for it first: no worker reads tuple memory after control leaves this function.
+// handed to on_rows(ids, seqs, submitted) while its tuples are valid, then released.
+// If on_rows stores a ticket >= 0 in `submitted` (a deferred pipeline submission that still reads the tuples; it
+// must store it right after the submission, before anything that can throw), the tuples of that fetch are freed
+// only after the NEXT fetch has been fetched and handed over and wait(ticket) has returned, so the staging of fetch
+// k runs on a pipeline worker while this backend fetches k+1.  Unwinding with a ticket outstanding -- held, or just
+// submitted when on_rows or the release of the previous fetch threw -- waits for the newest one first (fetches are
+// staged in submission order): no worker reads tuple memory after control leaves this function.
 template <class F, class W>
 void for_each_fetch_held(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows, W &&wait)
 {
@@ -151,17 +153,18 @@ void for_each_fetch_held(const char *sql, Oid nuclseq_oid, long fetch, F &&on_ro
     std::vector<int64_t> ids[2];
     std::vector<const NucleotideSequence *> seqs[2];   // alternate: the held fetch's pointers stay valid
     SPITupleTable *held_tt = nullptr;
-    int64_t held_ticket = -1;
+    int64_t held_ticket = -1, pending = -1;
     struct Guard {
         W &wait;
-        int64_t &ticket;
+        int64_t &held, &pending;
         ~Guard()
         {
-            if (ticket >= 0) {
-                try { wait(ticket); } catch (...) {}
+            const int64_t t = std::max(held, pending);
+            if (t >= 0) {
+                try { wait(t); } catch (...) {}
             }
         }
-    } guard{wait, held_ticket};
+    } guard{wait, held_ticket, pending};
     auto release_held = [&] {
         if (held_ticket >= 0) { const int64_t t = held_ticket; held_ticket = -1; wait(t); }
         if (held_tt) { SPITupleTable *t = held_tt; held_tt = nullptr; pg_call([&] { SPI_freetuptable(t); }); }
@@ -203,9 +206,10 @@ void for_each_fetch_held(const char *sql, Oid nuclseq_oid, long fetch, F &&on_ro
         });
         id_v.resize(kept);
         seq_v.resize(kept);
-        const int64_t ticket = on_rows(id_v, seq_v);
+        pending = -1;
+        on_rows(id_v, seq_v, pending);
         release_held();   // the previous fetch: staged by now or waited for
-        if (ticket >= 0) { held_tt = tt; held_ticket = ticket; }
+        if (pending >= 0) { held_tt = tt; held_ticket = pending; pending = -1; }
         else pg_call([&] { SPI_freetuptable(tt); });
     }
     release_held();
@@ -216,10 +220,8 @@ template <class F>
 void for_each_fetch(const char *sql, Oid nuclseq_oid, long fetch, F &&on_rows)
 {
     for_each_fetch_held(sql, nuclseq_oid, fetch,
-                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
-                            on_rows(ids, seqs);
-                            return (int64_t)-1;
-                        },
+                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs,
+                            int64_t &) { on_rows(ids, seqs); },
                         [](int64_t) {});
 }
 
@@ -437,13 +439,12 @@ void multi_search(FunctionCallInfo fcinfo)
     // Each fetch is staged by a pipeline worker (deferred submission) while this backend fetches the next one; its
     // tuples are freed once that staging is done (for_each_fetch_held).
     for_each_fetch_held(query_sql, nuclseq_oid, query_fetch_rows(),
-                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs) {
+                        [&](const std::vector<int64_t> &ids, const std::vector<const NucleotideSequence *> &seqs,
+                            int64_t &submitted) {
                             if ((int)ids_q.size() >= depth) drain_one();
-                            const int64_t ticket =
-                                index.submit_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt, true);
+                            submitted = index.submit_rows(seqs.data(), (int32_t)seqs.size(), true, &ci.opt, true);
                             ids_q.push_back(ids);
                             st.reads += (long long)seqs.size();
-                            return ticket;
                         },
                         [&](int64_t ticket) { index.wait_staged(ticket); });
     while (!ids_q.empty()) drain_one();

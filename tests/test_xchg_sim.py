@@ -43,3 +43,12 @@ def test_failure_on_one_rank_stops_every_rank(sim, world, lanes, rounds, fr, fl,
     assert rc == 0 and "OK (failure propagated)" in out, out
     tag = f"rank {fr} lane {fl} round {fk} failed"
     assert sum(1 for line in out.splitlines() if line.startswith("rank ") and tag in line) == world, out
+
+
+@pytest.mark.parametrize("world,lanes,rounds,fl,fk", [(2, 1, 4, 0, 1), (4, 1, 5, 0, 2), (3, 2, 4, 1, 1)])
+def test_rank0_receive_failure_does_not_hang(sim, world, lanes, rounds, fl, fk):
+    """a lane whose batch waits on a send rank 0 never matched publishes nothing; the other
+    ranks' exchange threads must give up (Transport::poll's deadline) instead of waiting forever.  One lane and
+    several rounds is the shape where no other wait of the exchange thread has a deadline."""
+    rc, out = _run(sim, world, lanes, rounds, 0, fl, fk, "recv")
+    assert rc == 0 and "OK (receive failure, no hang)" in out, out

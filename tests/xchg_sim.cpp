@@ -12,8 +12,12 @@
 //     at the offsets the Core computed (Parts), byte for byte -- ragged ranks, zero-read and zero-hit ranks,
 //     the staged (host-resident view) branch;
 //   * a batch failure on one rank stops every rank at the same (round, lane) with an error naming it, and nothing
-//     hangs (every wait in the transport has a deadline that fails the run instead).
-// Usage: xchg_sim <world> <lanes> <rounds> [fail_rank fail_lane fail_round]
+//     hangs (every wait in the transport has a deadline that fails the run instead);
+//   * a lane's next round waits for its previous send to be matched (batch_resume blocks, as the batch stream's
+//     wait on the RCCL `sent` event does), and when rank 0's receive fails locally (mode "recv") the other ranks'
+//     exchange threads, waiting for a lane that can never publish, give up through Transport::poll's deadline.
+//   Aborts are local to a rank (ncclCommAbort does not wake a peer).
+// Usage: xchg_sim <world> <lanes> <rounds> [fail_rank fail_lane fail_round [recv]]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -34,6 +38,7 @@ using namespace bsq::xchg;
 
 constexpr int64_t HIT = 72;   // sizeof(bsq_hit)
 constexpr double DEADLINE_S = 20.0;
+constexpr double POLL_DEADLINE_S = 3.0;   // the exchange thread's wait for a lane to publish (BSQ_XCHG_TIMEOUT_S)
 
 // ---- the records a (rank, lane, round) produces: deterministic, ragged, some empty ----
 struct Gen {
@@ -72,30 +77,33 @@ struct Fabric {
     int world;
     std::mutex mu;
     std::condition_variable cv;
-    bool aborted = false;
+    std::vector<char> aborted;   // per rank
     std::vector<std::string> violations;
     // all-gathers by issue index: lane + headers per rank
     struct AG { int lane = -1; int arrived = 0; std::vector<int64_t> hdr; };
     std::map<int64_t, AG> ag;
     // per source rank: FIFO of sends to rank 0 (lane, bytes)
     std::vector<std::deque<std::pair<int, std::vector<uint8_t>>>> q;
+    // per (source rank, lane): sends issued and sends matched by rank 0's receive
+    std::map<std::pair<int, int>, int64_t> issued, matched;
     std::atomic<int64_t> staged{0}, sends{0}, recvs{0};
-    explicit Fabric(int w) : world(w), q((size_t)w) {}
+    explicit Fabric(int w) : world(w), aborted((size_t)w, 0), q((size_t)w) {}
     void violate(const std::string &m) { std::lock_guard<std::mutex> lk(mu); violations.push_back(m); }
-    template <class P> bool wait(std::unique_lock<std::mutex> &lk, P pred, std::string &err, const char *what)
+    template <class P> bool wait(int rank, std::unique_lock<std::mutex> &lk, P pred, std::string &err, const char *what)
     {
-        if (!cv.wait_for(lk, std::chrono::duration<double>(DEADLINE_S), [&] { return aborted || pred(); })) {
+        if (!cv.wait_for(lk, std::chrono::duration<double>(DEADLINE_S), [&] { return aborted[(size_t)rank] || pred(); })) {
             err = std::string("deadline: ") + what + " never matched (a deadlock on real RCCL)";
             return false;
         }
-        if (aborted && !pred()) { err = "aborted"; return false; }
+        if (aborted[(size_t)rank] && !pred()) { err = "aborted"; return false; }
         return true;
     }
 };
 
 class FakeTransport final : public Transport {
   public:
-    FakeTransport(Fabric &f, int rank, int lanes) : f_(f), rank_(rank), recv_buf_((size_t)lanes) {}
+    FakeTransport(Fabric &f, int rank, int lanes, int fail_lane = -1, int fail_round = -1)
+        : f_(f), rank_(rank), recv_buf_((size_t)lanes), n_recv_((size_t)lanes, 0), fail_lane_(fail_lane), fail_round_(fail_round) {}
     int world() const override { return f_.world; }
     int rank() const override { return rank_; }
     int all_gather(int lane, const int64_t mine[4], int64_t *all, std::string &err) override
@@ -111,7 +119,7 @@ class FakeTransport final : public Transport {
         ++a.arrived;
         f_.cv.notify_all();
         const int64_t me = n_ag_++;
-        if (!f_.wait(lk, [&] { return f_.ag[me].arrived == f_.world; }, err, "an all-gather")) return -3;
+        if (!f_.wait(rank_, lk, [&] { return f_.ag[me].arrived == f_.world; }, err, "an all-gather")) return -3;
         memcpy(all, f_.ag[me].hdr.data(), (size_t)f_.world * 32);
         return 0;
     }
@@ -130,19 +138,24 @@ class FakeTransport final : public Transport {
         if (p.n_cigar) memcpy(w.data() + p.off_bytes() + p.hits_bytes(), r.cig, (size_t)p.cig_bytes());
         std::lock_guard<std::mutex> lk(f_.mu);
         f_.q[(size_t)rank_].emplace_back(lane, std::move(w));
+        ++f_.issued[{rank_, lane}];
         ++f_.sends;
         f_.cv.notify_all();
         return 0;
     }
     int recv(int lane, const std::vector<Parts> &parts, const std::vector<int64_t> &at, int64_t total, std::string &err) override
     {
+        if (lane == fail_lane_ && n_recv_[(size_t)lane] == fail_round_) { err = "injected receive failure"; return -3; }
+        ++n_recv_[(size_t)lane];
         std::vector<uint8_t> &buf = recv_buf_[(size_t)lane];
         buf.assign((size_t)total, 0xEE);
         for (int k = 1; k < f_.world; ++k) {
             std::unique_lock<std::mutex> lk(f_.mu);
-            if (!f_.wait(lk, [&] { return !f_.q[(size_t)k].empty(); }, err, "a receive")) return -3;
+            if (!f_.wait(rank_, lk, [&] { return !f_.q[(size_t)k].empty(); }, err, "a receive")) return -3;
             auto item = std::move(f_.q[(size_t)k].front());
             f_.q[(size_t)k].pop_front();
+            ++f_.matched[{k, item.first}];
+            f_.cv.notify_all();
             lk.unlock();
             const Parts &p = parts[(size_t)k];
             if (item.first != lane || (int64_t)item.second.size() != p.payload()) {
@@ -160,11 +173,24 @@ class FakeTransport final : public Transport {
         }
         return 0;
     }
-    int batch_resume(int, std::string &) override { return 0; }
+    // the RCCL transport makes the batch stream wait on the lane's `sent` event: the batch's next round cannot start
+    // before its previous send has been matched.  No deadline here, as on the device: only an abort releases it.
+    int batch_resume(int lane, std::string &err) override
+    {
+        std::unique_lock<std::mutex> lk(f_.mu);
+        f_.cv.wait(lk, [&] { return f_.aborted[(size_t)rank_] || f_.matched[{rank_, lane}] >= f_.issued[{rank_, lane}]; });
+        if (f_.matched[{rank_, lane}] < f_.issued[{rank_, lane}]) { err = "aborted while waiting for the lane's send"; return -3; }
+        return 0;
+    }
+    int poll(double waited_s, std::string &err) override
+    {
+        if (waited_s > POLL_DEADLINE_S) { err = "timed out waiting for a local batch"; return -3; }
+        return 0;
+    }
     void abort() override
     {
         std::lock_guard<std::mutex> lk(f_.mu);
-        f_.aborted = true;
+        f_.aborted[(size_t)rank_] = 1;
         f_.cv.notify_all();
     }
     const std::vector<uint8_t> &received(int lane) const { return recv_buf_[(size_t)lane]; }
@@ -175,6 +201,8 @@ class FakeTransport final : public Transport {
     int64_t n_ag_ = 0;
     std::vector<uint8_t> staging_;
     std::vector<std::vector<uint8_t>> recv_buf_;
+    std::vector<int> n_recv_;   // receives issued per lane (= rounds)
+    int fail_lane_, fail_round_;
 };
 
 // rank 0's view of lane `i` after round `k`: every other rank's parts, byte for byte
@@ -204,6 +232,7 @@ int main(int argc, char **argv)
     if (argc < 4) { fprintf(stderr, "usage: xchg_sim world lanes rounds [fail_rank fail_lane fail_round]\n"); return 2; }
     const int W = atoi(argv[1]), L = atoi(argv[2]), R = atoi(argv[3]);
     const int fr = argc > 6 ? atoi(argv[4]) : -1, fl = argc > 6 ? atoi(argv[5]) : -1, fk = argc > 6 ? atoi(argv[6]) : -1;
+    const bool recv_mode = argc > 7 && !strcmp(argv[7], "recv");   // rank 0's receive of (fl, fk) fails locally
     Fabric fab(W);
     std::vector<int> rc((size_t)W, 0);
     std::vector<std::string> err((size_t)W);
@@ -211,7 +240,7 @@ int main(int argc, char **argv)
     std::vector<std::string> why((size_t)W);
     std::mutex view_mu;
     auto rank_main = [&](int r) {
-        FakeTransport t(fab, r, L);
+        FakeTransport t(fab, r, L, recv_mode && r == 0 ? fl : -1, recv_mode && r == 0 ? fk : -1);
         Core core(t, L, HIT);
         std::vector<Gen> cur((size_t)L);
         auto produce = [&](int i, int k, Records &rec) -> int {
@@ -224,7 +253,7 @@ int main(int argc, char **argv)
                     if (!bad_view[0]) { bad_view[0] = 1; why[0] = w; }
                 }
             }
-            if (r == fr && i == fl && k == fk) return -3;
+            if (!recv_mode && r == fr && i == fl && k == fk) return -3;
             cur[(size_t)i] = gen(r, i, k);
             const Gen &g = cur[(size_t)i];
             rec.n_reads = g.n_reads; rec.n_hits = g.n_hits; rec.n_cigar = g.n_cigar;
@@ -250,6 +279,13 @@ int main(int argc, char **argv)
         for (int r = 0; r < W; ++r) if (rc[(size_t)r]) return 1;
         if (fab.sends.load() != (int64_t)(W - 1) * L * R || fab.recvs.load() != fab.sends.load()) return 1;
         printf("OK\n");
+        return 0;
+    }
+    if (recv_mode) {   // rank 0 names its receive; every other rank stops too (all-gather deadline or poll deadline)
+        if (!rc[0] || err[0].find("injected receive failure") == std::string::npos) { printf("rank 0 did not report its receive\n"); return 1; }
+        for (int r = 1; r < W; ++r)
+            if (!rc[(size_t)r]) { printf("rank %d did not stop\n", r); return 1; }
+        printf("OK (receive failure, no hang)\n");
         return 0;
     }
     // failure injected at (fr, fl, fk): every rank fails, naming it; nothing of a later (round, lane) was sent
