@@ -778,6 +778,7 @@ def main() -> int:
         nx = ctypes.c_void_p()
         hb.phase = "joining the exchange communicator"
         N.check(L.bsq_xchg_create(world, rank, gpu, idb, S, ctypes.byref(nx)))
+        N.check(L.bsq_xchg_set_index(nx, idx))   # rank 0 expands the received wire records with its anns
     elif dist is not None:
         from bioseqdb_amd import dist as D
         xchg = D.RecordExchange(device=xdev)

@@ -148,6 +148,9 @@ SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _P]),
     "bsq_xchg_finish": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "bsq_xchg_view": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Hits)]),
+    "bsq_xchg_set_index": (ctypes.c_int, [_P, _P]),
+    "bsq_xchg_wire_check": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                           ctypes.POINTER(ctypes.c_int64)]),
     "bsq_group_segments": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.POINTER(Hits)), ctypes.POINTER(ctypes.c_int32),
                                           ctypes.c_int]),
     "bsq_pipeline_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P)]),

@@ -20,6 +20,7 @@
 #include "bsq_device.h"
 #include "dev_common.h"
 #include "../../include/bsq.h"
+#include "bsq_internal.h"
 
 namespace bsq {
 
@@ -2226,6 +2227,38 @@ hipError_t launch_pack(hipStream_t st, int n, const SlotView &mv, const SlotView
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, st, n, mv, rv, retry_slot, off_hits, off_cig, ann_off,
                        ann_id, out, out_cig, read_base, cig_base);
     return hipGetLastError();
+}
+
+// The exchange's wire form (bsq_internal.h WireHit): one thread per read writes its hit count and its hits' 32-B
+// records; the read holding the batch's first hit writes the header {read_base, cig_base}.
+__global__ void k_wire_pack(int32_t n_reads, const int64_t *off, const bsq_hit *hits, uint8_t *off_part, WireHit *wire)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_reads) return;
+    const int64_t a = off[i], b = off[i + 1];
+    reinterpret_cast<int32_t *>(off_part + kWireHead)[i] = (int32_t)(b - a);
+    if (a == off[0] && b > a) {   // the first read with hits: its first hit is hits[0]
+        const bsq_hit &h = hits[0];
+        reinterpret_cast<int64_t *>(off_part)[0] = (int64_t)h.read_index - i;
+        reinterpret_cast<int64_t *>(off_part)[1] = (int64_t)h.cigar_off;
+    }
+    for (int64_t g = a; g < b; ++g) {
+        const bsq_hit &h = hits[g - off[0]];
+        WireHit w;
+        w.rb = h.rb; w.len = (int32_t)(h.re - h.rb); w.qb = h.qb; w.qe = h.qe; w.score = h.score; w.rid = h.rid;
+        w.ncig = h.n_cigar | (uint32_t)(h.is_primary != 0) << 29 | (uint32_t)(h.is_secondary != 0) << 30 |
+                 (uint32_t)(h.is_reverse != 0) << 31;
+        wire[g - off[0]] = w;
+    }
+}
+
+int launch_wire_pack(void *st, int32_t n_reads, const int64_t *off, const bsq_hit *hits, uint8_t *off_part, WireHit *wire)
+{
+    hipStream_t s = static_cast<hipStream_t>(st);
+    if (hipMemsetAsync(off_part, 0, kWireHead, s) != hipSuccess) return BSQ_E_HIP;
+    if (n_reads > 0)
+        hipLaunchKernelGGL(k_wire_pack, dim3((n_reads + 255) / 256), dim3(256), 0, s, n_reads, off, hits, off_part, wire);
+    return hipGetLastError() == hipSuccess ? BSQ_OK : BSQ_E_HIP;
 }
 
 __global__ void k_add_base(int64_t *v, int n, int64_t base)

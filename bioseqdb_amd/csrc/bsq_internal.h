@@ -62,6 +62,27 @@ struct BatchRecords {
     int64_t n_hits = 0, n_cigar = 0;
 };
 BatchRecords batch_records(const bsq_batch *b);
+
+// The exchange's wire form of one lane-round's records (bsq_xchg, exchange.cpp).  A bsq_hit is 72 B; on the wire a hit
+// is 32 B: ref_id and the three ref_match_* fields follow from rid, rb and the length through the index's anns
+// (bsq_api k_pack), re = rb + len, read_index from the read's position and cigar_off from the prefix of n_cigar over
+// the hits (the batch-wide arrays k_pack fills: read_index = read_base + i, cigar_off = cig_base + that prefix).
+// The read offsets travel as one int32 hit count per read after a 16-B header {read_base, cig_base}.  CIGAR words
+// travel as they are.  Rank 0 takes the compact form over its PCIe link and expands it on the host.
+struct WireHit {
+    int64_t rb;
+    int32_t len, qb, qe, score, rid;
+    uint32_t ncig;   // n_cigar | is_primary << 29 | is_secondary << 30 | is_reverse << 31
+};
+static_assert(sizeof(WireHit) == 32, "wire hit layout");
+constexpr int64_t kWireHead = 16;   // {int64 read_base, int64 cig_base} before the int32 counts
+inline int64_t wire_off_bytes(int64_t n_reads) { return kWireHead + 4 * n_reads; }
+// device: the wire form of n_reads reads' records (off: n_reads + 1 batch offsets, hits) into off_part (header +
+// counts) and wire (n_hits); on stream `st` (hipStream_t)
+int launch_wire_pack(void *st, int32_t n_reads, const int64_t *off, const bsq_hit *hits, uint8_t *off_part, WireHit *wire);
+// host: the records back, byte for byte as the sender's k_pack wrote them (padding zeroed); ann_off/ann_id of the index
+void wire_expand(const uint8_t *off_part, const WireHit *wire, int32_t n_reads, const int64_t *ann_off,
+                 const int64_t *ann_id, int64_t n_anns, int64_t *read_off, bsq_hit *hits);
 // bsq_batch_render_nuclseqs into the batch's own pinned buffers: *out / *out_off are borrowed until the next
 // render or run of the batch (the pipeline hands them out until the slot is released).
 int batch_render_cols(bsq_batch *b, const void *const *reads, const uint8_t **out, const int64_t **out_off);

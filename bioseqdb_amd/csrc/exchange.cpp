@@ -23,12 +23,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/bsq.h"
 #include "bsq_internal.h"
+#include "bsq_index.h"
 #include "exchange_core.h"
 
 extern "C" void bsq_internal_set_error(const char *msg);
@@ -71,8 +73,10 @@ struct Lane {
     hipEvent_t packed = nullptr;     // on bs: the round's records are final
     hipEvent_t sent = nullptr;       // on xs: the send buffers may be overwritten
     bool has_sent = false;
-    uint8_t *send_dev = nullptr;     // staging of a host-resident view (a round with retried reads)
+    uint8_t *send_dev = nullptr;     // the round's wire form (bsq_internal.h WireHit): header + counts, hits, CIGAR words
     int64_t send_cap = 0;
+    uint8_t *stage_dev = nullptr;    // a host-resident view (a round with retried reads) copied to HBM before packing
+    int64_t stage_cap = 0;
     uint8_t *recv_dev = nullptr;     // rank 0: every other rank's parts
     int64_t recv_cap = 0;
     uint8_t *recv_host = nullptr;    // rank 0: the same, pinned (the caller's view of the last round)
@@ -156,26 +160,38 @@ class RcclTransport final : public bsq::xchg::Transport {
         return BSQ_OK;
     }
 
+    // The round's records go out in the wire form (bsq_internal.h WireHit, 32 B per hit + 4 B per read instead of
+    // 72 + 8): k_wire_pack on the exchange stream turns the batch's packed records into it, and rank 0 expands it on
+    // its host (bsq_xchg_view).  The bytes through rank 0's one PCIe link are what the 8-rank exchange funnels.
     int send(int li, const Records &r, const Parts &p, std::string &err) override
     {
         Lane &l = lanes[(size_t)li];
         THIP(hipSetDevice(device_));
+        if (p.total() > l.send_cap) { if (const int rc = sync_xs(err)) return rc; }   // the old buffer may be in flight
+        if (const int rc = grow(l.send_dev, l.send_cap, p.total(), false, err)) return rc;
         const void *off = r.off, *hits = r.hits, *cig = r.cig;
-        if (!r.on_device) {   // the view is in pinned host memory: stage it in HBM first (same stream)
-            if (p.total() > l.send_cap) { if (const int rc = sync_xs(err)) return rc; }   // the old buffer may be in flight
-            if (const int rc = grow(l.send_dev, l.send_cap, p.total(), false, err)) return rc;
-            THIP(hipMemcpyAsync(l.send_dev, r.off, (size_t)p.off_bytes(), hipMemcpyHostToDevice, xs));
-            if (p.n_hits) THIP(hipMemcpyAsync(l.send_dev + p.o_hit(), r.hits, (size_t)p.hits_bytes(), hipMemcpyHostToDevice, xs));
+        if (!r.on_device) {   // the view is in pinned host memory: copy it to HBM first (same stream)
+            const int64_t ob = (r.n_reads + 1) * 8, need = bsq::xchg::al(ob) + r.n_hits * (int64_t)sizeof(bsq_hit);
+            if (need > l.stage_cap) { if (const int rc = sync_xs(err)) return rc; }
+            if (const int rc = grow(l.stage_dev, l.stage_cap, need, false, err)) return rc;
+            THIP(hipMemcpyAsync(l.stage_dev, r.off, (size_t)ob, hipMemcpyHostToDevice, xs));
+            if (p.n_hits) THIP(hipMemcpyAsync(l.stage_dev + bsq::xchg::al(ob), r.hits, (size_t)(r.n_hits * sizeof(bsq_hit)),
+                                              hipMemcpyHostToDevice, xs));
             if (p.n_cigar) THIP(hipMemcpyAsync(l.send_dev + p.o_cig(), r.cig, (size_t)p.cig_bytes(), hipMemcpyHostToDevice, xs));
-            off = l.send_dev; hits = l.send_dev + p.o_hit(); cig = l.send_dev + p.o_cig();
-            // the batch's next run may regrow (free) the pinned view these copies read
-            if (const int rc = sync_xs(err)) return rc;
-        } else {   // straight from the batch's packed arrays: the send waits for the batch stream's pack
+            off = l.stage_dev; hits = l.stage_dev + bsq::xchg::al(ob); cig = l.send_dev + p.o_cig();
+        } else {   // straight from the batch's packed arrays: the pack waits for the batch stream's pack
             THIP(hipStreamWaitEvent(xs, l.packed, 0));
         }
+        if (bsq::launch_wire_pack(xs, (int32_t)p.n_reads, static_cast<const int64_t *>(off), static_cast<const bsq_hit *>(hits),
+                                  l.send_dev, reinterpret_cast<bsq::WireHit *>(l.send_dev + p.o_hit())) != BSQ_OK) {
+            err = "k_wire_pack launch failed";
+            return BSQ_E_HIP;
+        }
+        // the batch's next run may regrow (free) the pinned view the staging copies read
+        if (!r.on_device) { if (const int rc = sync_xs(err)) return rc; }
         TNCCL(ncclGroupStart());
-        TNCCL(ncclSend(off, (size_t)p.off_bytes(), ncclUint8, 0, comm, xs));
-        if (p.n_hits) TNCCL(ncclSend(hits, (size_t)p.hits_bytes(), ncclUint8, 0, comm, xs));
+        TNCCL(ncclSend(l.send_dev, (size_t)p.off_bytes(), ncclUint8, 0, comm, xs));
+        if (p.n_hits) TNCCL(ncclSend(l.send_dev + p.o_hit(), (size_t)p.hits_bytes(), ncclUint8, 0, comm, xs));
         if (p.n_cigar) TNCCL(ncclSend(cig, (size_t)p.cig_bytes(), ncclUint8, 0, comm, xs));
         TNCCL(ncclGroupEnd());
         THIP(hipEventRecord(l.sent, xs));
@@ -223,7 +239,7 @@ class RcclTransport final : public bsq::xchg::Transport {
         if (xs && !aborted) hipStreamSynchronize(xs);
         if (comm) ncclCommDestroy(comm);
         for (Lane &l : lanes) {
-            hipFree(l.send_dev); hipFree(l.recv_dev); hipHostFree(l.recv_host);
+            hipFree(l.send_dev); hipFree(l.stage_dev); hipFree(l.recv_dev); hipHostFree(l.recv_host);
             if (l.packed) hipEventDestroy(l.packed);
             if (l.sent) hipEventDestroy(l.sent);
         }
@@ -237,6 +253,11 @@ class RcclTransport final : public bsq::xchg::Transport {
 struct bsq_xchg {
     std::unique_ptr<RcclTransport> t;
     std::unique_ptr<bsq::xchg::Core> core;
+    // rank 0: the index's anns (bsq_xchg_set_index) and the views expanded from the wire form, per (lane, rank)
+    std::vector<int64_t> ann_off, ann_id;
+    struct View { int64_t round = -1; std::vector<int64_t> off; std::vector<bsq_hit> hits; };
+    mutable std::mutex view_mu;
+    mutable std::vector<View> views;   // lane * world + rank
 };
 
 extern "C" int bsq_xchg_unique_id(void *id)
@@ -274,7 +295,8 @@ extern "C" int bsq_xchg_create(int world, int rank, int device, const void *id, 
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
     XNCCL(ncclCommInitRank(&t.comm, world, u, rank));
-    x->core.reset(new bsq::xchg::Core(t, lanes, (int64_t)sizeof(bsq_hit)));
+    x->core.reset(new bsq::xchg::Core(t, lanes, (int64_t)sizeof(bsq::WireHit), 4, bsq::kWireHead));
+    x->views.resize((size_t)lanes * (size_t)world);
     *out = x.release();
     return BSQ_OK;
 }
@@ -348,14 +370,122 @@ extern "C" int bsq_xchg_view(const bsq_xchg *x, int lane, int src_rank, bsq_hits
     if (x->t->rank_ != 0 || src_rank == 0) return fail(BSQ_E_INVALID, "rank 0 holds the other ranks' records (its own are in its batches)");
     const bsq::xchg::LaneState &ls = x->core->lane(lane);
     if (!ls.rounds) return fail(BSQ_E_INVALID, "no round exchanged yet");
+    if (x->ann_off.empty()) return fail(BSQ_E_INVALID, "bsq_xchg_view: no index set (bsq_xchg_set_index) to expand the records with");
     const Parts &p = ls.parts[(size_t)src_rank];
     uint8_t *h = x->t->lanes[(size_t)lane].recv_host + ls.at[(size_t)src_rank];
+    std::lock_guard<std::mutex> lk(x->view_mu);
+    bsq_xchg::View &v = x->views[(size_t)lane * (size_t)x->t->world_ + (size_t)src_rank];
+    if (v.round != ls.rounds) {   // expanded once per exchanged round
+        v.off.resize((size_t)p.n_reads + 1);
+        v.hits.resize((size_t)std::max<int64_t>(p.n_hits, 1));
+        bsq::wire_expand(h, reinterpret_cast<const bsq::WireHit *>(h + p.o_hit()), (int32_t)p.n_reads, x->ann_off.data(),
+                         x->ann_id.data(), (int64_t)x->ann_off.size(), v.off.data(), v.hits.data());
+        v.round = ls.rounds;
+    }
     *out = bsq_hits{};
     out->n_reads = (int32_t)p.n_reads;
     out->n_hits = p.n_hits;
-    out->read_off = reinterpret_cast<int64_t *>(h);
-    out->hits = reinterpret_cast<bsq_hit *>(h + p.o_hit());
+    out->read_off = v.off.data();
+    out->hits = v.hits.data();
     out->n_cigar = p.n_cigar;
     out->cigar = reinterpret_cast<uint32_t *>(h + p.o_cig());
     return BSQ_OK;
+}
+
+extern "C" int bsq_xchg_set_index(bsq_xchg *x, const bsq_index *idx)
+{
+    if (!x || !idx) return fail(BSQ_E_INVALID, "invalid argument");
+    const std::vector<bsq::Ann> &a = idx->h.anns;
+    x->ann_off.assign(std::max<size_t>(a.size(), 1), 0);
+    x->ann_id.assign(std::max<size_t>(a.size(), 1), 0);
+    for (size_t i = 0; i < a.size(); ++i) { x->ann_off[i] = a[i].offset; x->ann_id[i] = a[i].id; }
+    return BSQ_OK;
+}
+
+namespace bsq {
+
+void wire_expand(const uint8_t *off_part, const WireHit *wire, int32_t n_reads, const int64_t *ann_off, const int64_t *ann_id,
+                 int64_t n_anns, int64_t *read_off, bsq_hit *hits)
+{
+    int64_t read_base = 0, cig = 0;
+    memcpy(&read_base, off_part, 8);
+    memcpy(&cig, off_part + 8, 8);
+    const uint8_t *cnt = off_part + kWireHead;
+    int64_t g = 0;
+    read_off[0] = 0;
+    for (int32_t i = 0; i < n_reads; ++i) {
+        int32_t c;
+        memcpy(&c, cnt + 4 * (size_t)i, 4);
+        for (int32_t k = 0; k < c; ++k, ++g) {
+            const WireHit &w = wire[g];
+            bsq_hit &b = hits[g];
+            memset(&b, 0, sizeof b);   // k_pack zeroes the padding: records compare byte for byte
+            const int64_t roff = w.rid >= 0 && w.rid < n_anns ? ann_off[w.rid] : 0;
+            b.ref_id = w.rid >= 0 && w.rid < n_anns ? ann_id[w.rid] : 0;
+            b.rb = w.rb;
+            b.re = w.rb + w.len;
+            b.ref_match_start = (int32_t)(b.rb - roff);
+            b.ref_match_end = (int32_t)(b.re - roff);
+            b.ref_match_len = w.len;
+            b.qb = w.qb; b.qe = w.qe; b.score = w.score; b.rid = w.rid;
+            b.is_primary = (uint8_t)(w.ncig >> 29 & 1); b.is_secondary = (uint8_t)(w.ncig >> 30 & 1);
+            b.is_reverse = (uint8_t)(w.ncig >> 31 & 1);
+            b.read_index = (int32_t)(read_base + i);
+            b.n_cigar = w.ncig & ((1u << 29) - 1);
+            b.cigar_off = (uint32_t)cig;
+            cig += b.n_cigar;
+        }
+        read_off[i + 1] = g;
+    }
+}
+
+}  // namespace bsq
+
+// The wire form checked on one GPU (the exchange's send half runs only with peers): the batch's last records through
+// the same k_wire_pack the send path launches, back to the host, expanded as rank 0's views are, and compared byte
+// for byte with the batch's own view.  *wire_bytes / *raw_bytes: what one (round, lane) puts on the link now / as
+// bsq_hit records with int64 offsets.
+extern "C" int bsq_xchg_wire_check(bsq_batch *b, const bsq_index *idx, int64_t *wire_bytes, int64_t *raw_bytes,
+                                   int64_t *mismatches)
+{
+    if (!b || !idx || !mismatches) return fail(BSQ_E_INVALID, "invalid argument");
+    const bsq::BatchRecords r = bsq::batch_records(b);
+    const bsq_hits *view = bsq_batch_hits(b);
+    if (!view) return fail(BSQ_E_INVALID, "the batch has no records");
+    XHIP(hipSetDevice(r.device));
+    hipStream_t st = static_cast<hipStream_t>(r.stream);
+    Parts p;
+    p.n_reads = r.n_reads; p.n_hits = r.n_hits; p.n_cigar = r.n_cigar;
+    p.hit_bytes = (int64_t)sizeof(bsq::WireHit); p.off_per_read = 4; p.off_fixed = bsq::kWireHead;
+    const int64_t ob = (r.n_reads + 1) * 8, hb = r.n_hits * (int64_t)sizeof(bsq_hit);
+    uint8_t *dev = nullptr, *stage = nullptr;
+    std::vector<uint8_t> host((size_t)p.o_cig());
+    auto done = [&](int rc) { hipFree(dev); hipFree(stage); return rc; };
+    if (hipMalloc(&dev, (size_t)std::max<int64_t>(p.o_cig(), 1)) != hipSuccess) return done(fail(BSQ_E_NOMEM, "hipMalloc"));
+    const void *off = r.off, *hits = r.hits;
+    if (!r.on_device) {
+        if (hipMalloc(&stage, (size_t)(bsq::xchg::al(ob) + std::max<int64_t>(hb, 1))) != hipSuccess) return done(fail(BSQ_E_NOMEM, "hipMalloc"));
+        if (hipMemcpyAsync(stage, r.off, (size_t)ob, hipMemcpyHostToDevice, st) != hipSuccess ||
+            (hb && hipMemcpyAsync(stage + bsq::xchg::al(ob), r.hits, (size_t)hb, hipMemcpyHostToDevice, st) != hipSuccess))
+            return done(fail(BSQ_E_HIP, "staging copy"));
+        off = stage; hits = stage + bsq::xchg::al(ob);
+    }
+    if (bsq::launch_wire_pack(st, (int32_t)p.n_reads, static_cast<const int64_t *>(off), static_cast<const bsq_hit *>(hits),
+                              dev, reinterpret_cast<bsq::WireHit *>(dev + p.o_hit())) != BSQ_OK)
+        return done(fail(BSQ_E_HIP, "k_wire_pack"));
+    if (hipMemcpyAsync(host.data(), dev, host.size(), hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return done(fail(BSQ_E_HIP, "wire copy"));
+    std::vector<int64_t> ann_off(std::max<size_t>(idx->h.anns.size(), 1), 0), ann_id(ann_off.size(), 0);
+    for (size_t i = 0; i < idx->h.anns.size(); ++i) { ann_off[i] = idx->h.anns[i].offset; ann_id[i] = idx->h.anns[i].id; }
+    std::vector<int64_t> ro((size_t)p.n_reads + 1);
+    std::vector<bsq_hit> hx((size_t)std::max<int64_t>(p.n_hits, 1));
+    bsq::wire_expand(host.data(), reinterpret_cast<const bsq::WireHit *>(host.data() + p.o_hit()), (int32_t)p.n_reads,
+                     ann_off.data(), ann_id.data(), (int64_t)ann_off.size(), ro.data(), hx.data());
+    int64_t bad = 0;
+    for (int64_t i = 0; i <= p.n_reads; ++i) bad += ro[(size_t)i] != view->read_off[i] - view->read_off[0];
+    for (int64_t g = 0; g < p.n_hits; ++g) bad += memcmp(&hx[(size_t)g], &view->hits[g], sizeof(bsq_hit)) != 0;
+    *mismatches = bad;
+    if (wire_bytes) *wire_bytes = p.payload();
+    if (raw_bytes) *raw_bytes = ob + hb + p.cig_bytes();
+    return done(BSQ_OK);
 }

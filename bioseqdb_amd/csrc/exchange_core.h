@@ -41,11 +41,13 @@ namespace xchg {
 constexpr int64_t kAlign = 256;
 inline int64_t al(int64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
-// One rank's records of one round: read offsets (n_reads + 1 int64), hits (n_hits x hit_bytes), CIGAR words
-// (n_cigar u32); each part 256-B aligned inside the rank's slice of rank 0's receive buffer.
+// One rank's records of one round: read offsets (n_reads x off_per_read + off_fixed bytes: the RCCL transport's wire
+// form is a 16-B header and one int32 count per read, the host simulation sends n_reads + 1 int64 offsets), hits
+// (n_hits x hit_bytes), CIGAR words (n_cigar u32); each part 256-B aligned inside the rank's slice of rank 0's
+// receive buffer.
 struct Parts {
-    int64_t n_reads = 0, n_hits = 0, n_cigar = 0, hit_bytes = 0;
-    int64_t off_bytes() const { return (n_reads + 1) * 8; }
+    int64_t n_reads = 0, n_hits = 0, n_cigar = 0, hit_bytes = 0, off_per_read = 8, off_fixed = 8;
+    int64_t off_bytes() const { return n_reads * off_per_read + off_fixed; }
     int64_t hits_bytes() const { return n_hits * hit_bytes; }
     int64_t cig_bytes() const { return n_cigar * 4; }
     int64_t o_hit() const { return al(off_bytes()); }
@@ -99,7 +101,8 @@ using Produce = std::function<int(int, int, Records &)>;
 
 class Core {
   public:
-    Core(Transport &t, int lanes, int64_t hit_bytes) : t_(t), hit_bytes_(hit_bytes), lanes_((size_t)lanes)
+    Core(Transport &t, int lanes, int64_t hit_bytes, int64_t off_per_read = 8, int64_t off_fixed = 8)
+        : t_(t), hit_bytes_(hit_bytes), off_per_read_(off_per_read), off_fixed_(off_fixed), lanes_((size_t)lanes)
     {
         for (LaneState &l : lanes_) { l.parts.resize((size_t)t.world()); l.at.resize((size_t)t.world()); }
     }
@@ -192,7 +195,7 @@ class Core {
                 for (int r = 0; r < W; ++r) {
                     Parts &p = l.parts[(size_t)r];
                     p.n_reads = all[(size_t)r * 4]; p.n_hits = all[(size_t)r * 4 + 1]; p.n_cigar = all[(size_t)r * 4 + 2];
-                    p.hit_bytes = hit_bytes_;
+                    p.hit_bytes = hit_bytes_; p.off_per_read = off_per_read_; p.off_fixed = off_fixed_;
                     l.at[(size_t)r] = total;
                     if (r != 0) total += p.total();
                 }
@@ -234,7 +237,7 @@ class Core {
         return rc < 0 ? rc : -3;
     }
     Transport &t_;
-    int64_t hit_bytes_;
+    int64_t hit_bytes_, off_per_read_, off_fixed_;
     std::vector<LaneState> lanes_;
     double wait_ms_ = 0;
     bool aborted_ = false;

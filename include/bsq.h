@@ -240,8 +240,16 @@ int bsq_batch_run_rounds_x(bsq_batch *const *batches, int n, const bsq_opts *opt
  * received (rank 0) or sent (others) over all rounds; *wait_ms: host time the batch threads spent exchanging. */
 int bsq_xchg_finish(bsq_xchg *x, int64_t *bytes_moved, double *wait_ms);
 /* Rank 0: the last round's records of lane `lane` from rank src_rank > 0 (read_index and cigar_off local to that
- * rank's batch), borrowed until the next round or free. */
+ * rank's batch), borrowed until the next round or free.  They travel in a compact wire form (32 B per hit and 4 B
+ * per read instead of 72 + 8: ref_id, re, ref_match_*, read_index and cigar_off are implied) and are expanded here,
+ * byte for byte what the sender's batch holds, with the anns of the index given to bsq_xchg_set_index. */
 int bsq_xchg_view(const bsq_xchg *x, int lane, int src_rank, bsq_hits *out);
+/* Rank 0: the index (the one every rank aligns against) whose anns expand the received records. */
+int bsq_xchg_set_index(bsq_xchg *x, const bsq_index *idx);
+/* One GPU: the batch's last records through the exchange's wire form and back (the send path's device pack, the
+ * view's host expansion), compared byte for byte with the batch's view (*mismatches: differing read offsets and
+ * records).  *wire_bytes / *raw_bytes: the round's bytes on the link in the wire form / as bsq_hit + int64 offsets. */
+int bsq_xchg_wire_check(bsq_batch *b, const bsq_index *idx, int64_t *wire_bytes, int64_t *raw_bytes, int64_t *mismatches);
 
 /* ---- Pipelined cursor fetches (replaces the fetch-align-materialise loop of
  * nuclseq_multi_search_bwa, extension.cpp:156-195 + 362-370, which leaves the device idle between fetches).
