@@ -393,6 +393,42 @@ def cpu_baseline(O, oi, oo, codes, offs, n_reads, threads, seeding, seconds, fir
             "value": round(sample / med, 1), "value_1thread": round(n1 / med1, 1)}
 
 
+def exchange_budget(L, idx, batches, step_ms: float) -> dict:
+    """The torchrun exchange's ingress at rank 0 (the rows of every rank reach the caller's
+    tuplestore, bioseqdb/extension.cpp:362-370), budgeted from one GPU: this rank's records of one step in the wire
+    form the exchange sends (bsq_xchg_wire_check: the send path's device pack, rank 0's host expansion, compared
+    byte for byte with the batch's view) and as bsq_hit records, and the measured pinned D2H rate of one PCIe link --
+    rank 0's link carries the 7 peers' wire records plus its own records at 8 GPUs."""
+    import torch
+    wire = raw = bad = 0
+    for b in batches:
+        wb, rb, mm = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        N.check(L.bsq_xchg_wire_check(b, idx, ctypes.byref(wb), ctypes.byref(rb), ctypes.byref(mm)))
+        wire += wb.value
+        raw += rb.value
+        bad += mm.value
+    nbytes, reps = 256 << 20, 8
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    rate = reps * nbytes / (time.perf_counter() - t)
+    del src, dst
+    out = {"bytes_per_step_rank_wire": wire, "bytes_per_step_rank_raw": raw,
+           "wire_saving": round(1 - wire / raw, 3) if raw else None, "wire_roundtrip_mismatches": bad,
+           "d2h_pinned_GBps": round(rate / 1e9, 2), "step_ms_1gpu": round(step_ms, 3)}
+    for n in (2, 4, 8):   # rank 0's link: (n - 1) peers' wire records + its own records, per step
+        ing = (n - 1) * wire + raw
+        out[f"rank0_ingress_{n}gpu"] = {"bytes_per_step": ing, "d2h_ms_per_step": round(ing / rate * 1e3, 3),
+                                        "frac_of_step": round(ing / rate * 1e3 / step_ms, 3),
+                                        "raw_records_d2h_ms": round(n * raw / rate * 1e3, 3)}
+    return out
+
+
 def make_roofline(dom, di, stage_ms, stage_bytes, reads_per_launch, iso, iso_reads, per_read, tr, S):
     """The bench line's `roofline` for the dominant stage: the lone launch over all the step's reads when there
     is one (the kernel's own time), with the shared-CU figure of the timed concurrent batches beside it.
@@ -947,6 +983,10 @@ def main() -> int:
                     N.check(L.bsq_xchg_view(nx, k, r, ctypes.byref(v)))
                     ck += gpu_checksum_vec(v, lo_k[k + 1] - lo_k[k], lo_k[k])
                 result["checksums"].append(ck & 0xFFFFFFFFFFFFFFFF)
+
+    if world == 1 and not cfg["seeding"] and not args.timed_only:
+        hb.phase = "exchange budget"
+        result["exchange_budget"] = exchange_budget(L, idx, batches, elapsed / args.steps * 1e3)
 
     # ---- N > 1: the last rank's records as rank 0 received them, against the CPU oracle on a sample ----
     if nx is not None and world > 1 and rank == 0 and not args.no_cpu_baseline:
