@@ -1042,7 +1042,42 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
         // [beg, end), last non-zero in [beg, end]) are tracked here from the values being stored; every
         // stored h and e is >= 0, so "non-zero" is (h | e) != 0.
         int nzf = beg < end ? end : beg, nzl = -1;   // (the serial scan's start values)
-        if (beg < end) {
+        if (EH::kRing && pre && beg < end) {
+            // LDS ring: each cell first stores the previous cell's column (deferred by one cell), then reads column
+            // j + 2, then computes column j from values read two cells earlier.  Every LDS operation of a cell is thus
+            // issued before its arithmetic, and the wait at the next cell's top finds them done -- with the store
+            // last in the cell (the loop above), each trip waited out a whole LDS store latency.  The deferred store
+            // starts as a rewrite of column beg's own old value; reads of columns end + 1 (stale slot) and query
+            // index qlen + 1 (inside the staged rows or the ring) are never used.
+            typename EH::Cur c0 = eh.cur(beg), c1 = eh.adv(c0);
+            int2 p0 = eh.at(c0), p1 = eh.at(c1);
+            int q0 = query(beg), q1 = query(beg + 1);
+            typename EH::Cur sc = c0;
+            int2 sv = p0;
+#pragma unroll 2
+            for (j = beg; j < end; ++j) {
+                eh.put(sc, sv);
+                const typename EH::Cur c2 = eh.adv(c1);
+                const int2 p2 = eh.at(c2);
+                const int q2 = query(j + 2);
+                int h, M = p0.x, e = p0.y;
+                const int hx = h1;
+                M = M ? M + (int)__builtin_amdgcn_ubfe(prof, (uint32_t)q0, 4u) - 8 : 0;
+                h = M > e ? M : e;
+                h = h > f ? h : f;
+                h1 = h;
+                mj = m > h ? mj : j;
+                m = m > h ? m : h;
+                t = M - oe_del; t = t > 0 ? t : 0;
+                e -= e_del; e = e > t ? e : t;
+                sc = c0; sv = make_int2(hx, e);
+                if ((hx | e) != 0) { nzl = j; nzf = nzf < j ? nzf : j; }
+                t = M - oe_ins; t = t > 0 ? t : 0;
+                f -= e_ins; f = f > t ? f : t;
+                p0 = p1; p1 = p2; q0 = q1; q1 = q2; c0 = c1; c1 = c2;
+            }
+            eh.put(sc, sv);
+        } else if (beg < end) {
             typename EH::Cur cj = eh.cur(beg);
             int2 p = eh.at(cj);
             int qj = query(beg);

@@ -39,6 +39,7 @@ def _ref():
 def test_wire_roundtrip_device_records():
     ref = _ref()
     pi, _ = build_pair([t.decode() for t in ref.texts()], ids=[11, -3, 7, 1 << 40, 5])
+    pi.upload()
     reads = synth.make_reads(ref, 20_000, seed=41)
     n_hits, wire, raw, bad = _wire_check(pi, reads, first_call=9)
     assert n_hits > 18_000 and bad == 0
@@ -49,6 +50,7 @@ def test_wire_roundtrip_staged_host_view(monkeypatch):
     monkeypatch.setenv("BSQ_TEST_TINY_CAPS", "1")   # reads through the retry pass: the records are a host view
     ref = _ref()
     pi, _ = build_pair([t.decode() for t in ref.texts()])
+    pi.upload()
     reads = synth.make_reads(ref, 800, seed=43)
     n_hits, wire, raw, bad = _wire_check(pi, reads)
     assert n_hits > 700 and bad == 0
