@@ -296,6 +296,99 @@ DEV int ksw_global2_reg(const Score sc, int qlen, int q_off, int q_start, int q_
     return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
 }
 
+// ksw_global2 for bands of 65..128 columns, row state in registers with TWO columns per lane (lane l owns band columns
+// c0 = 2l and c1 = 2l + 1).  The rows are ksw_global2_reg's: the F recurrence is one wave scan over the lanes' pair
+// maxima, F(c0) = max(F0 - c0*e, max_{c<c0} (tf_c - (c0-1-c)e)) and F(c1) = max(F(c0) - e, tf(c0)); a band slide by
+// s = 0 moves H one column right (c1 of lane l-1 into c0 of lane l), s = 1 moves E and the query one column left.
+// It replaces ksw_global2_w's LDS row (two 64-column chunks per row for these bands, an LDS round trip per chunk and a
+// workgroup fence per row).  Same cells, same traceback bytes.
+template <bool ZL>
+DEV int ksw_global2_reg2(const Score sc, int qlen, int q_off, int q_start, int q_dir, const DIndex &ix, int64_t t_start,
+                         int t_dir, int tlen, int o_del, int e_del, int o_ins, int e_ins, int w, int n_col, int z_off,
+                         uint8_t *zg, uint64_t &cells)
+{
+    const int l = lane_id(), c0 = 2 * l, c1 = c0 + 1;
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    uint32_t tw = 0;   // target, 16 bases per lane (tlen <= 1024)
+    for (int k = 0; k < 16; ++k) {
+        const int i = l * 16 + k;
+        if (i < tlen) tw |= (uint32_t)ref_at(ix, t_start + (int64_t)t_dir * i) << (2 * k);
+    }
+    uint32_t qpk = 0;   // query, 8 bases per lane (qlen <= 512)
+    for (int k = 0; k < 8; ++k) {
+        const int j = l * 8 + k;
+        const uint32_t v = j < qlen ? (uint32_t)g_lds_dp[q_off + q_start + q_dir * j] : 4u;
+        qpk |= v << (4 * k);
+    }
+    int qv0 = c0 < qlen ? g_lds_dp[q_off + q_start + q_dir * c0] : 4;
+    int qv1 = c1 < qlen ? g_lds_dp[q_off + q_start + q_dir * c1] : 4;
+    int Hd0 = c0 == 0 ? 0 : (c0 <= w ? -(o_ins + e_ins * c0) : MINUS_INF_W);
+    int Hd1 = c1 <= w ? -(o_ins + e_ins * c1) : MINUS_INF_W;
+    int E0 = MINUS_INF_W, E1 = MINUS_INF_W;
+    int beg = 0, last_end = 0, width = 0, h0 = 0, h1 = 0;
+    for (int i = 0; i < tlen; ++i) {
+        const int tb = (int)((uint32_t)__builtin_amdgcn_readlane((int)tw, i >> 4) >> (2 * (i & 15))) & 3;
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        width = end - beg;
+        const bool a0 = c0 < width, a1 = c1 < width;
+        const int m0 = Hd0 + sc(tb, qv0), m1 = Hd1 + sc(tb, qv1);
+        const int tf0 = m0 - oe_ins, tf1 = m1 - oe_ins;
+        const int g0 = a0 ? tf0 + c0 * e_ins : NEG_SCAN, g1 = a1 ? tf1 + c1 * e_ins : NEG_SCAN;
+        const int ex = wave_excl_max(g0 > g1 ? g0 : g1);
+        int f0 = MINUS_INF_W - c0 * e_ins;
+        if (l > 0) { const int fs = ex - (c0 - 1) * e_ins; f0 = f0 > fs ? f0 : fs; }
+        int f1 = f0 - e_ins;
+        f1 = f1 > tf0 ? f1 : tf0;
+        int d0 = m0 >= E0 ? 0 : 1, d1 = m1 >= E1 ? 0 : 1;
+        h0 = m0 >= E0 ? m0 : E0;
+        h1 = m1 >= E1 ? m1 : E1;
+        d0 = h0 >= f0 ? d0 : 2;
+        d1 = h1 >= f1 ? d1 : 2;
+        h0 = h0 >= f0 ? h0 : f0;
+        h1 = h1 >= f1 ? h1 : f1;
+        const int te0 = m0 - oe_del, e20 = E0 - e_del, te1 = m1 - oe_del, e21 = E1 - e_del;
+        d0 |= e20 > te0 ? 1 << 2 : 0;
+        d1 |= e21 > te1 ? 1 << 2 : 0;
+        const int en0 = e20 > te0 ? e20 : te0, en1 = e21 > te1 ? e21 : te1;
+        d0 |= f0 - e_ins > tf0 ? 2 << 4 : 0;
+        d1 |= f1 - e_ins > tf1 ? 2 << 4 : 0;
+        if (a0) {
+            if (ZL) g_lds_dp[z_off + i * n_col + c0] = (uint8_t)d0;
+            else zg[i * n_col + c0] = (uint8_t)d0;
+        }
+        if (a1) {
+            if (ZL) g_lds_dp[z_off + i * n_col + c1] = (uint8_t)d1;
+            else zg[i * n_col + c1] = (uint8_t)d1;
+        }
+        cells += (uint64_t)width;
+        last_end = end;
+        const int beg_next = i + 1 > w ? i + 1 - w : 0;
+        if (beg_next == beg) {   // (only while beg == 0: column -1 is the boundary)
+            Hd0 = wave_shr1(h1, -(o_del + e_del * (i + 1)));
+            Hd1 = h0;
+            E0 = a0 ? en0 : MINUS_INF_W;
+            E1 = a1 ? en1 : MINUS_INF_W;
+        } else {
+            Hd0 = h0;
+            Hd1 = h1;
+            const int es = wave_shl1(en0, MINUS_INF_W);
+            E0 = a1 ? en1 : MINUS_INF_W;
+            E1 = c1 + 1 < width ? es : MINUS_INF_W;
+            const int jn = beg_next + 127;   // column entering lane 63's second slot
+            const int qn = jn < qlen ? (int)((uint32_t)__builtin_amdgcn_readlane((int)qpk, jn >> 3) >> (4 * (jn & 7))) & 15 : 4;
+            const int qs = wave_shl1(qv0, qn);
+            qv0 = qv1;
+            qv1 = qs;
+        }
+        beg = beg_next;
+    }
+    if (tlen > 0 && last_end == qlen) {
+        const int cw = width - 1;
+        return __builtin_amdgcn_readlane((cw & 1) ? h1 : h0, cw >> 1);
+    }
+    return qlen == 0 ? 0 : (qlen <= w ? -(o_ins + e_ins * qlen) : MINUS_INF_W);
+}
+
 // traceback of a z matrix held in LDS (offset) or global memory; libbwa push_cigar semantics.
 // G lanes cooperate (a DPP row, a 32-lane segment or the wave; gl = lane in the group, gbase = the
 // group's first lane): in the match state the next G cells of the diagonal are read at once and a
@@ -397,6 +490,17 @@ DEV int gen_cigar2_w(const DIndex &ix, const DOpts &o, int w_, int q_off, int qb
                                                 nullptr, cells)
                         : ksw_global2_reg<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
                                                  (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
+            if (zl) traceback_w<true, 64>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
+            else traceback_w<false, 64>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
+        } else if (n_col <= 128 && rlen < (int64_t)l_query + w && rlen <= 1024 && l_query <= 512) {
+            // two columns per lane (the bands of 65..128 columns the group kernels defer here)
+            if ((int64_t)n_col * rlen > zcap) { ovf = true; return 0; }
+            const bool zl = z_off >= 0;
+            *score = zl ? ksw_global2_reg2<true>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
+                                                 (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, z_off,
+                                                 nullptr, cells)
+                        : ksw_global2_reg2<false>(score_of(o), l_query, q_off, qa.start, qa.dir, ix, ta.start, ta.dir,
+                                                  (int)rlen, o.o_del, o.e_del, o.o_ins, o.e_ins, w, n_col, 0, z, cells);
             if (zl) traceback_w<true, 64>(l_query, (int)rlen, w, n_col, z_off, nullptr, cig, cap, ncig, ovf);
             else traceback_w<false, 64>(l_query, (int)rlen, w, n_col, 0, z, cig, cap, ncig, ovf);
         } else {
