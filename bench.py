@@ -399,7 +399,6 @@ def exchange_budget(L, idx, batches, step_ms: float) -> dict:
     form the exchange sends (bsq_xchg_wire_check: the send path's device pack, rank 0's host expansion, compared
     byte for byte with the batch's view) and as bsq_hit records, and the measured pinned D2H rate of one PCIe link --
     rank 0's link carries the 7 peers' wire records plus its own records at 8 GPUs."""
-    import torch
     wire = raw = bad = 0
     for b in batches:
         wb, rb, mm = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -407,17 +406,21 @@ def exchange_budget(L, idx, batches, step_ms: float) -> dict:
         wire += wb.value
         raw += rb.value
         bad += mm.value
+    # the HIP runtime libbsq already uses (torch's lazy CUDA init is not safe here after the batches' HIP use)
+    hip = ctypes.CDLL("libamdhip64.so.7")   # libbsq's DT_NEEDED: the same loaded runtime
     nbytes, reps = 256 << 20, 8
-    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    dst.copy_(src, non_blocking=True)
-    torch.cuda.synchronize()
+    src, dst = ctypes.c_void_p(), ctypes.c_void_p()
+    if hip.hipMalloc(ctypes.byref(src), ctypes.c_size_t(nbytes)) or hip.hipHostMalloc(ctypes.byref(dst), ctypes.c_size_t(nbytes), 0):
+        raise RuntimeError("exchange budget: HIP allocation failed")
+    D2H = 2   # hipMemcpyDeviceToHost
+    hip.hipMemcpy(dst, src, ctypes.c_size_t(nbytes), D2H)
     t = time.perf_counter()
     for _ in range(reps):
-        dst.copy_(src, non_blocking=True)
-    torch.cuda.synchronize()
+        if hip.hipMemcpy(dst, src, ctypes.c_size_t(nbytes), D2H):
+            raise RuntimeError("exchange budget: hipMemcpy failed")
     rate = reps * nbytes / (time.perf_counter() - t)
-    del src, dst
+    hip.hipFree(src)
+    hip.hipHostFree(dst)
     out = {"bytes_per_step_rank_wire": wire, "bytes_per_step_rank_raw": raw,
            "wire_saving": round(1 - wire / raw, 3) if raw else None, "wire_roundtrip_mismatches": bad,
            "d2h_pinned_GBps": round(rate / 1e9, 2), "step_ms_1gpu": round(step_ms, 3)}
