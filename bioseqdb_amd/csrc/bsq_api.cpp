@@ -61,7 +61,7 @@ hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_
 bool wide_z32(const DIndex &);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
-hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int, bool, uint64_t *);
+hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
 struct RenderHole { int64_t beg, end; uint32_t order; uint32_t amb; };
 struct RenderView {
     const bsq_hit *hits; const uint32_t *cigar; int64_t n_hits; const uint8_t *pac; int64_t l_pac;
@@ -322,21 +322,6 @@ struct IndexMeta {   // fixed header of the metadata blob; followed by Ann[n_ann
     uint64_t table_bytes[T_N];
 };
 
-// The compact k-mer table (bsq_device.h DIndex::kmer_compact): u32 rows whose row numbers fit 28 bits (text up to
-// ~134 Mbp per strand: C1-C3); BSQ_KMER_COMPACT=0 keeps the 16-B entries (A/B)
-static bool kmer_compact_for(uint64_t seq_len, int wide)
-{
-    const char *e = getenv("BSQ_KMER_COMPACT");
-    return !wide && seq_len + 1 < (1ull << 28) && !(e && *e == '0');
-}
-// entries of a compact table of depth K: levels 1..K, 4^L codes + 1 sentinel each
-static uint64_t kmer_compact_words(int K)
-{
-    uint64_t w = 0;
-    for (int L = 1; L <= K; ++L) w += (1ull << (2 * L)) + 1;
-    return w;
-}
-
 static int kmer_depth(uint64_t seq_len, bool wide)
 {
     if (seq_len == 0) return 0;
@@ -347,8 +332,7 @@ static int kmer_depth(uint64_t seq_len, bool wide)
     // 2.9 GB table).  Depth 13 only for 64-bit rows, the kernels that preload 13 levels
     // (and the only ones measured there): u32 rows of a 256 Mbp - 2 Gbp text stay at 10, where u32 kernels preload
     // 11 levels and read deeper ones one per step (slower at C3: 11.3-12.1 ms against 10.45).
-    // The compact table (4 B per string) holds depth 11 in the cache footprint of the 16-B depth 10 (22 MB).
-    const int kmax = wide && seq_len / 2 > (256ull << 20) ? 13 : kmer_compact_for(seq_len, wide) ? 11 : 10;
+    const int kmax = wide && seq_len / 2 > (256ull << 20) ? 13 : 10;
     int K = 0;
     while (K < kmax && (1ull << (2 * (K + 1))) <= seq_len) ++K;
     // BSQ_KMER_K: 0 disables; up to 15 (the kernels preload levels <= 11 and read deeper levels one per step;
@@ -372,8 +356,7 @@ static void table_sizes(const HostIndex &h, uint64_t bytes[T_N], int &K, int &wi
     bytes[T_SA] = (h.seq_len + 1) * (wide ? 8 : 4);
     bytes[T_PAC] = h.pac.size() + 16;
     K = kmer_depth(h.seq_len, wide != 0);
-    bytes[T_KMER] = !K ? 0 : kmer_compact_for(h.seq_len, wide) ? kmer_compact_words(K) * 4
-                                                                : (((uint64_t)1 << (2 * (K + 1))) - 4) / 3 * (wide ? 32 : 16);
+    bytes[T_KMER] = K ? (((uint64_t)1 << (2 * (K + 1))) - 4) / 3 * (wide ? 32 : 16) : 0;
 }
 
 static void set_view(DeviceIndex *d, const IndexMeta &m)
@@ -397,7 +380,6 @@ static void set_view(DeviceIndex *d, const IndexMeta &m)
                                : nullptr;
     v.kmer = m.kmer_k ? d->kmer : nullptr;
     v.kmer_k = m.kmer_k;
-    v.kmer_compact = m.kmer_k && kmer_compact_for(m.seq_len, m.wide) ? 1 : 0;
 }
 
 static IndexMeta meta_of(const HostIndex &h)
@@ -497,13 +479,9 @@ static int upload_impl(bsq_index *idx, int device, const bsq_table *ext)
     // 100 Mbp; 64-bit rows: 32-B entries, 179 MB); BSQ_KMER_K overrides, 0 disables
     if (m.kmer_k > 0) {
         d->view.kmer = d->kmer;
-        const bool kc = kmer_compact_for(m.seq_len, m.wide);
-        uint64_t bad = 0;
-        HIPCHK(launch_kmer_build(nullptr, d->view, d->kmer, m.kmer_k, kc, &bad));
+        HIPCHK(launch_kmer_build(nullptr, d->view, d->kmer, m.kmer_k));
         HIPCHK(hipDeviceSynchronize());
-        if (bad) { set_err("compact k-mer table: %llu entries fail the check", (unsigned long long)bad); return BSQ_E_HIP; }
         d->view.kmer_k = m.kmer_k;
-        d->view.kmer_compact = kc;
     }
     return BSQ_OK;
 }
@@ -583,12 +561,8 @@ extern "C" int bsq_index_build_device(bsq_index *idx, int device)
     set_view(d, mv);
     if (m2.kmer_k > 0) {
         d->view.kmer = d->kmer;
-        const bool kc = kmer_compact_for(m2.seq_len, m2.wide);
-        uint64_t bad = 0;
-        if (launch_kmer_build(nullptr, d->view, d->kmer, m2.kmer_k, kc, &bad) != hipSuccess) { set_err("k-mer table build"); return fail(BSQ_E_HIP); }
-        if (bad) { set_err("compact k-mer table: %llu entries fail the check", (unsigned long long)bad); return fail(BSQ_E_HIP); }
+        if (launch_kmer_build(nullptr, d->view, d->kmer, m2.kmer_k) != hipSuccess) { set_err("k-mer table build"); return fail(BSQ_E_HIP); }
         d->view.kmer_k = m2.kmer_k;
-        d->view.kmer_compact = kc;
     }
     if (hipDeviceSynchronize() != hipSuccess) { set_err("GPU index build: %s", hipGetErrorString(hipGetLastError())); return fail(BSQ_E_HIP); }
     return BSQ_OK;

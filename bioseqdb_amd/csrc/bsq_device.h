@@ -72,12 +72,7 @@ struct DIndex {
     const OccBlock32 *occ32;  // 64-base rank blocks (absolute counts for u32 rows, superblock-relative otherwise)
     const SupBlock *sup;      // 64-bit rows: superblock counts (after the blocks in the occ32 table); else nullptr
     int32_t wide;             // 1: 64-bit rows (seq_len >= 2^32, or forced by BSQ_FORCE_WIDE)
-    // 1: the k-mer table is the compact form (u32 rows with seq_len < 2^28): one u32 per string, x[0] in the low 28
-    // bits and in the top 4 the number of suffixes of T$ shorter than |S| that sort between S and the next string of
-    // its length; every level followed by one sentinel word.  x[2] = x0(next) - x0(S) - that count (intervals of the
-    // strings of one length, in code order, tile the suffix array apart from those short suffixes) and x[1] =
-    // x0(revcomp S) (T = pac || revcomp(pac)): a quarter of the 16-B entry's bytes
-    int32_t kmer_compact;
+    int32_t pad2;
 };
 
 // mem_opt_t fields the path reads (mem_opt_init defaults + bioseqdb overrides).

@@ -22,18 +22,6 @@ namespace bsq {
 
 #define DEV __device__ __forceinline__
 
-// first entry of the k-mer table level for strings of length L: (4^L - 4) / 3 (compact table: + L - 1 sentinels)
-DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
-// code of the reverse complement of the L-base string `code` (first base most significant): complement, then the
-// 2-bit fields in reverse order
-DEV uint32_t rc_code(uint32_t code, int L)
-{
-    uint32_t r = __builtin_bitreverse32(~code);
-    r = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
-    return r >> (32 - 2 * L);
-}
-constexpr uint32_t KC_MASK = (1u << 28) - 1;
-
 template <typename X>
 struct FM {
     const OccBlock *occ;
@@ -41,56 +29,35 @@ struct FM {
     const SupBlock *sup;       // X = u64: superblock counts
     const uint4 *kt;   // k-mer interval table (bsq_device.h DIndex::kmer), depth K (0 = none)
     int K;
-    bool kc;           // compact table (DIndex::kmer_compact; set from a kernel template constant, so folded)
-    // Strings of length L with code `code`.  Full entries: (x[0], x[2], x[1], 0) as 4 x u32 (16 B) or, for 64-bit rows,
-    // 4 x u64 (32 B); (x[0], x[2]) first, so the backward phase (which never reads x[1]) takes one 8-B (16-B) load per
-    // entry.  Compact entries (u32 rows): x[0] and x[2] from one 8-B load of the string's word and the next one, x[1]
-    // from the reverse complement's word.
-    DEV const uint32_t *kcw(int L, uint32_t code) const
-    {
-        return reinterpret_cast<const uint32_t *>(kt) + koff(L) + (uint32_t)(L - 1) + code;
-    }
+    // table entry idx: (x[0], x[2], x[1], 0) as 4 x u32 (16 B) or, for 64-bit rows, 4 x u64 (32 B); (x[0], x[2])
+    // first, so the backward phase (which never reads x[1]) takes one 8-B (16-B) load per entry
     template <typename Z>
-    DEV void kget02(int L, uint32_t code, X &a0, Z &a2) const
+    DEV void kget(uint32_t idx, X &a0, X &a1, Z &a2) const
     {
         if constexpr (sizeof(X) == 4) {
-            if (kc) {
-                uint2 v;
-                __builtin_memcpy(&v, kcw(L, code), 8);   // 4-byte aligned: one global_load_dwordx2
-                a0 = v.x & KC_MASK;
-                a2 = (Z)((v.y & KC_MASK) - (v.x & KC_MASK) - (v.x >> 28));
-                return;
-            }
-            const uint2 e = reinterpret_cast<const uint2 *>(kt)[2 * (size_t)(koff(L) + code)];
-            a0 = e.x; a2 = (Z)e.y;
-        } else {
-            const ulonglong2 u = reinterpret_cast<const ulonglong2 *>(kt)[2 * (size_t)(koff(L) + code)];
-            a0 = u.x; a2 = (Z)u.y;
-        }
-    }
-    template <typename Z>
-    DEV void kget(int L, uint32_t code, X &a0, X &a1, Z &a2) const
-    {
-        if constexpr (sizeof(X) == 4) {
-            if (kc) {
-                a1 = *kcw(L, rc_code(code, L)) & KC_MASK;
-                kget02(L, code, a0, a2);
-                return;
-            }
-            const uint4 e = kt[koff(L) + code];
+            const uint4 e = kt[idx];
             a0 = e.x; a2 = (Z)e.y; a1 = e.z;
         } else {
-            const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(kt) + 2 * (size_t)(koff(L) + code);
+            const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(kt) + 2 * (size_t)idx;
             const ulonglong2 u = p[0], v = p[1];
             a0 = u.x; a2 = (Z)u.y; a1 = v.x;
         }
     }
-    DEV X kget1(int L, uint32_t code) const
+    template <typename Z>
+    DEV void kget02(uint32_t idx, X &a0, Z &a2) const
     {
         if constexpr (sizeof(X) == 4) {
-            if (kc) return *kcw(L, rc_code(code, L)) & KC_MASK;
-            return reinterpret_cast<const uint32_t *>(kt)[4 * (size_t)(koff(L) + code) + 2];
-        } else return reinterpret_cast<const uint64_t *>(kt)[4 * (size_t)(koff(L) + code) + 2];
+            const uint2 e = reinterpret_cast<const uint2 *>(kt)[2 * (size_t)idx];
+            a0 = e.x; a2 = (Z)e.y;
+        } else {
+            const ulonglong2 u = reinterpret_cast<const ulonglong2 *>(kt)[2 * (size_t)idx];
+            a0 = u.x; a2 = (Z)u.y;
+        }
+    }
+    DEV X kget1(uint32_t idx) const
+    {
+        if constexpr (sizeof(X) == 4) return reinterpret_cast<const uint32_t *>(kt)[4 * (size_t)idx + 2];
+        else return reinterpret_cast<const uint64_t *>(kt)[4 * (size_t)idx + 2];
     }
     X l2_0, l2_1, l2_2, l2_3, l2_4, primary;
     // the text T = pac || revcomp(pac) and its suffix array, for walking a unique interval along the text
@@ -301,6 +268,8 @@ DEV void ext_back2(const FM<X> &fm, X a0, Z a2, X b0, Z b2, bool da, bool hb, in
     }
 }
 
+// first entry of the k-mer table level for strings of length L: (4^L - 4) / 3
+DEV uint32_t koff(int L) { return ((1u << (2 * L)) - 4u) / 3u; }
 
 // The lane's list of (x0, x2, end) entries: entries e < cap in LDS (entry e at element offset e * stride,
 // lane-interleaved), the next gcap in this read's global spill area (lists longer than the LDS share
@@ -378,13 +347,13 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
         for (int t = 2; t <= KM; ++t) {
             if (nt == t - 1 && cb[t] < 4) {
                 fcode = fcode << 2 | (uint32_t)cb[t];
-                fm.kget02(t, fcode, e0[t], e2[t]);
+                fm.kget02(koff(t) + fcode, e0[t], e2[t]);
                 nt = t;
             }
         }
         if (nt >= 2) {
             nkm += (uint64_t)(nt - 1);
-            const X x1_last = fm.kget1(nt, fcode);
+            const X x1_last = fm.kget1(koff(nt) + fcode);
 #pragma unroll
             for (int t = 2; t <= KM; ++t) {
                 if (t <= nt && !stop) {
@@ -450,7 +419,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
             Z n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
-                fm.kget(i - x + 1, fcode, n0, n1, n2);
+                fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 != ik2) {
@@ -510,8 +479,8 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
                 const bool ta = La <= K, tb = hb && Lb <= K;
                 X ea0 = 0, eb0 = 0;
                 Z ea2 = 0, eb2 = 0;
-                if (ta) fm.kget02(La, wcode >> (2 * (K - La)), ea0, ea2);
-                if (tb) fm.kget02(Lb, wcode >> (2 * (K - Lb)), eb0, eb2);
+                if (ta) fm.kget02(koff(La) + (wcode >> (2 * (K - La))), ea0, ea2);
+                if (tb) fm.kget02(koff(Lb) + (wcode >> (2 * (K - Lb))), eb0, eb2);
                 nkm += (uint64_t)ta + (uint64_t)tb;
                 if (!ta || (hb && !tb)) ext_back2(fm, pa0, pa2, pb0, pb2, !ta, hb && !tb, c, oa0, oa2, ob0, ob2, nblk);
                 if (ta) { oa0 = ea0; oa2 = ea2; }
@@ -573,7 +542,7 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int 
             fcode = fcode << 2 | (uint32_t)c;
         }
         if (L > 1) {
-            fm.kget(L, fcode, ik0, ik1, ik2);
+            fm.kget(koff(L) + fcode, ik0, ik1, ik2);
             ++nkm;
         }
         i0 = x + L;
@@ -588,7 +557,7 @@ DEV int seed_strategy1_x(const FM<X> &fm, int len, Q q, int x, int min_len, int 
             Z n2;
             fcode = fcode << 2 | (uint32_t)cur;
             if (i - x + 1 <= fm.K) {
-                fm.kget(i - x + 1, fcode, n0, n1, n2);
+                fm.kget(koff(i - x + 1) + fcode, n0, n1, n2);
                 ++nkm;
             } else extend1(fm, ik1, ik0, ik2, c, n1, n0, n2, nblk);
             if (n2 < (Z)max_intv && i - x >= min_len) {
@@ -634,7 +603,7 @@ __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const 
 }
 
 // 4 waves per SIMD for u32 rows (16 one-wave blocks per CU, the LDS limit), 3 for 64-bit rows
-template <typename X, typename Z, typename Q, bool KC>
+template <typename X, typename Z, typename Q>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
@@ -663,7 +632,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
     fm.primary = (X)ix.primary;
     fm.kt = reinterpret_cast<const uint4 *>(ix.kmer);
     fm.K = ix.kmer_k;   // the table is built in the index's row width
-    fm.kc = KC;         // == ix.kmer_compact (the launch picks the instantiation)
     fm.pac = ix.pac; fm.l_pac = ix.l_pac; fm.sa32 = ix.sa32; fm.sa64 = ix.sa64;
     uint64_t nblk = 0, nkm = 0;
     // one read per lane; a grid smaller than the batch (BSQ_SMEM_GRID, the co-residency experiment) loops its waves
@@ -774,20 +742,19 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int L = cp.max_len;
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
-#define BSQ_SMEM_LAUNCH(X_, Z_, KC_)                                                                                    \
+#define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
     do {                                                                                                               \
         const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
         if (codes_t)                                                                                                   \
-            hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT, KC_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n, \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,      \
                                intv, n_intv, status, ctr, lcap, spill, gcap, L);                                       \
         else                                                                                                           \
-            hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *, KC_>), dim3(grid), dim3(T), sh, st, ix, o, cp,      \
-                               codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                       \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,    \
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                              \
     } while (0)
-    if (!ix.wide && ix.kmer_compact) BSQ_SMEM_LAUNCH(uint32_t, uint32_t, true);   // compact k-mer table (C1-C3)
-    else if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t, false);
-    else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t, false);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
-    else BSQ_SMEM_LAUNCH(uint64_t, uint64_t, false);
+    if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t);
+    else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
+    else BSQ_SMEM_LAUNCH(uint64_t, uint64_t);
 #undef BSQ_SMEM_LAUNCH
     return hipGetLastError();
 }
@@ -826,12 +793,11 @@ __global__ void k_kmer_level(DIndex ix, void *tabv, int L)
     fm.sup = ix.sup;
     fm.kt = reinterpret_cast<const uint4 *>(tabv);
     fm.K = 0;
-    fm.kc = false;   // the build runs on full entries (the compact table is derived from them)
     fm.l2_0 = (X)ix.L2[0]; fm.l2_1 = (X)ix.L2[1]; fm.l2_2 = (X)ix.L2[2];
     fm.l2_3 = (X)ix.L2[3]; fm.l2_4 = (X)ix.L2[4];
     fm.primary = (X)ix.primary;
     X x0, x1, x2;
-    fm.kget(L, (uint32_t)P, x0, x1, x2);
+    fm.kget((uint32_t)(koff(L) + P), x0, x1, x2);
     X o0[4], o2[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -849,80 +815,16 @@ __global__ void k_kmer_level(DIndex ix, void *tabv, int L)
     put(d + 3 * n, o0[3], x1_3, o2[3]);
 }
 
-// The compact table (bsq_device.h DIndex::kmer_compact) of level L from its full 16-B entries: word P < 4^L holds x0 and
-// the count of short suffixes between string P and P + 1 (x0(P + 1) - x0(P) - x2(P)); word 4^L is the sentinel
-// x0 + x2 of the last string.  Out-of-range values (x0 >= 2^28, a count above 15) are counted in *bad.
-__global__ void k_kmer_compact(const uint4 *full, uint32_t *kc, int L, unsigned long long *bad)
+// entry bytes: 16 (u32 rows) or 32 (64-bit rows)
+hipError_t launch_kmer_build(hipStream_t st, const DIndex &ix, uint32_t *tab, int K)
 {
-    const uint32_t n = 1u << (2 * L), P = blockIdx.x * blockDim.x + threadIdx.x;
-    if (P > n) return;
-    const uint4 *lv = full + koff(L);
-    uint32_t w;
-    bool ok;
-    if (P < n) {
-        const uint4 e = lv[P];
-        const uint32_t s = P + 1 < n ? lv[P + 1].x - e.x - e.y : 0u;
-        ok = e.x <= KC_MASK && s <= 15u;
-        w = e.x | s << 28;
-    } else {
-        const uint4 e = lv[n - 1];
-        w = e.x + e.y;
-        ok = w <= KC_MASK;
-    }
-    kc[koff(L) + (uint32_t)(L - 1) + P] = w;
-    if (!ok) atomicAdd(bad, 1ull);
-}
-
-// Every string of level L read back through the compact accessors against its full entry: x0 and x2 always, x1 (the
-// reverse complement's x0) for non-empty intervals -- the only ones whose x1 the kernels read.
-__global__ void k_kmer_check(const uint4 *full, const uint32_t *kc, int L, unsigned long long *bad)
-{
-    const uint32_t n = 1u << (2 * L), P = blockIdx.x * blockDim.x + threadIdx.x;
-    if (P >= n) return;
-    FM<uint32_t> fm{};
-    fm.kt = reinterpret_cast<const uint4 *>(kc);
-    fm.kc = true;
-    uint32_t a0, a1, a2;
-    fm.kget(L, P, a0, a1, a2);
-    const uint4 e = full[koff(L) + P];
-    if (a0 != e.x || a2 != e.y || (e.y != 0 && a1 != e.z)) atomicAdd(bad, 1ull);
-}
-
-// entry bytes: 16 (u32 rows) or 32 (64-bit rows); compact: 4 per string + a sentinel per level, built from a
-// temporary full table and checked against it entry by entry (*bad: entries that fail)
-hipError_t launch_kmer_build(hipStream_t st, const DIndex &ix, uint32_t *tab, int K, bool compact, uint64_t *bad)
-{
-    *bad = 0;
-    uint32_t *full = tab;
-    if (compact) {
-        hipError_t e = hipMalloc(&full, (size_t)((((uint64_t)1 << (2 * (K + 1))) - 4) / 3) * 16);
-        if (e != hipSuccess) return e;
-    }
     for (int L = 0; L < K; ++L) {
         const uint64_t n = L == 0 ? 4 : 1ull << (2 * L);
         const dim3 g((unsigned)((n + 255) / 256)), bl(256);
-        if (ix.wide) hipLaunchKernelGGL(k_kmer_level<uint64_t>, g, bl, 0, st, ix, (void *)full, L);
-        else hipLaunchKernelGGL(k_kmer_level<uint32_t>, g, bl, 0, st, ix, (void *)full, L);
+        if (ix.wide) hipLaunchKernelGGL(k_kmer_level<uint64_t>, g, bl, 0, st, ix, (void *)tab, L);
+        else hipLaunchKernelGGL(k_kmer_level<uint32_t>, g, bl, 0, st, ix, (void *)tab, L);
     }
-    if (!compact) return hipGetLastError();
-    unsigned long long *dbad = nullptr, hbad = 0;
-    hipError_t e = hipMalloc(&dbad, 8);
-    if (e == hipSuccess) e = hipMemsetAsync(dbad, 0, 8, st);
-    for (int L = 1; L <= K && e == hipSuccess; ++L) {
-        const uint32_t n = 1u << (2 * L);
-        hipLaunchKernelGGL(k_kmer_compact, dim3((n + 256) / 256), dim3(256), 0, st, reinterpret_cast<const uint4 *>(full), tab, L, dbad);
-    }
-    for (int L = 1; L <= K && e == hipSuccess; ++L) {
-        const uint32_t n = 1u << (2 * L);
-        hipLaunchKernelGGL(k_kmer_check, dim3((n + 255) / 256), dim3(256), 0, st, reinterpret_cast<const uint4 *>(full), tab, L, dbad);
-    }
-    if (e == hipSuccess) e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(&hbad, dbad, 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    hipFree(dbad);
-    hipFree(full);
-    *bad = hbad;
-    return e;
+    return hipGetLastError();
 }
 
 }  // namespace bsq
