@@ -1022,7 +1022,7 @@ def main() -> int:
 
         t_sub, sub_s = [0.0], [0.0]
 
-        def cursor(cols, deferred=True):
+        def cursor(cols, deferred=True, passes=passes):
             # deferred (the drop-in's loop since round 5, extension_bsq.cpp for_each_fetch_held): fetch k is staged by a
             # pipeline worker, and its tuples are "freed" after fetch k+1 is submitted and k's staging has finished;
             # copy: staged on the caller's thread inside bsq_pipeline_submit (round 4)
@@ -1077,6 +1077,11 @@ def main() -> int:
         rows_r, dt_r = cursor(0)
         sub_r = sub_s[0]
         rows_cc, dt_cc = cursor(1, deferred=False)
+        # the same loop over a 16M-read cursor (61 fetches): the pipeline's fill (the first fetch's staging and upload)
+        # and drain (the last fetches running with fewer beside them) amortised, as on a large table
+        long_passes = 16
+        rows_cl, dt_cl = cursor(1, passes=long_passes)
+        rows_rl, dt_rl = cursor(0, passes=long_passes)
         nr = passes * reads.n
         result["sql_cursor"] = {
             "reads": nr, "fetch_rows": fetch, "depth": depth,
@@ -1084,6 +1089,11 @@ def main() -> int:
             "same_row_count": rows_c == passes * n_hits and rows_r == passes * n_hits and rows_cc == passes * n_hits,
             "submit_s": [round(sub_c, 4), round(sub_r, 4)], "loop_s": [round(dt_c, 4), round(dt_r, 4)],
             "copy_staging_reads_per_s_with_columns": round(nr / dt_cc, 1),
+            "steady_state": {"reads": long_passes * reads.n,
+                             "reads_per_s_with_columns": round(long_passes * reads.n / dt_cl, 1),
+                             "reads_per_s_records_only": round(long_passes * reads.n / dt_rl, 1),
+                             "same_row_count": rows_cl == long_passes * n_hits and rows_rl == long_passes * n_hits,
+                             "loop_s": [round(dt_cl, 4), round(dt_rl, 4)]},
             "note": "bsq_pipeline over fetches of host nuclseq varlenas (deferred submissions: staged by the pipeline's "
                     "workers while the caller submits the next fetch, then upload, alignment, D2H, and with columns the "
                     "two nuclseq columns of every row on the GPU), as extension_bsq.cpp's cursor loop runs it, over a "
