@@ -957,28 +957,31 @@ struct EhL {   // offset-based so the accesses stay in the LDS address space (ds
 };
 
 #define EXT_LDS_COLS 64   // ring columns (a power of two)
-// 64-column ring in LDS (column j at slot j & 63, lane-interleaved): ksw_extend2 only touches columns [beg, end] of the
-// current row and beg never decreases, so the ring holds every live column while the window stays under 64 columns;
-// columns are given their initial value when the band first reaches them.  A wider window sets *ovf (the read is
-// re-run by the large-capacity retry pass).  A slot is one word: h (13 bits) | e (13 bits) << 13 | q4 << 26, where q4 is
-// the column's query base (4 * code) written when the column is initialised -- the cell loop reads h, e and its query
-// base in one LDS read (the launch checks h, e < 2^13).
+// 64-column ring of u16 pairs in LDS (column j at slot j & 63, lane-interleaved): ksw_extend2 only touches
+// columns [beg, end] of the current row and beg never decreases, so the ring holds every live column while
+// the window stays under 64 columns; columns are given their initial value when the band first reaches
+// them.  A wider window sets *ovf (the read is re-run by the large-capacity retry pass).
 struct EhRing {
     static constexpr bool kRing = true;
-    static constexpr uint32_t HM = (1u << 13) - 1, QM = 0xfc000000u;
     bool *ovf;
     int base;
-    DEV uint32_t &word(int j) const { return g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64]; }
-    DEV void init(int j, int h, int q4) const { word(j) = (uint32_t)h | (uint32_t)q4 << 26; }   // e = 0
-    DEV void set(int j, int2 v) const { uint32_t &w = word(j); w = (uint32_t)v.x | (uint32_t)v.y << 13 | (w & QM); }
+    DEV int2 get(int j) const { uint32_t v = g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64]; return make_int2((int)(v & 0xffffu), (int)(v >> 16)); }
+    DEV void set(int j, int2 v) const { g_lds_eh[base + (j & (EXT_LDS_COLS - 1)) * 64] = (uint32_t)v.x | ((uint32_t)v.y << 16); }
     // Cell-loop cursor: the slot's byte offset 4 * (lane + (j & 63) * 64) (base is the lane, < 64, and the ring is the
     // first 16 KB of the dynamic LDS), advanced by one add and one and per column instead of recomputed for every
-    // access.
+    // access (the loop reads column j + 1 and stores column j: the store's slot is the previous read's).
     using Cur = uint32_t;
     DEV Cur cur(int j) const { return 4u * ((uint32_t)base + ((uint32_t)j & (EXT_LDS_COLS - 1)) * 64u); }
     DEV Cur adv(Cur c) const { return (c + 256u) & (EXT_LDS_COLS * 256u - 1u); }
-    DEV uint32_t at(Cur c) const { return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(g_lds_eh) + c); }
-    DEV void put(Cur c, uint32_t w) const { *reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(g_lds_eh) + c) = w; }
+    DEV int2 at(Cur c) const
+    {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(g_lds_eh) + c);
+        return make_int2((int)(v & 0xffffu), (int)(v >> 16));
+    }
+    DEV void put(Cur c, int2 v) const
+    {
+        *reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(g_lds_eh) + c) = (uint32_t)v.x | ((uint32_t)v.y << 16);
+    }
 };
 
 // Query accessors whose values are pre-scaled codes (4 * code) with readable padding one column past either
@@ -999,12 +1002,7 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
     const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
     auto init_h = [&](int jj) { return jj == 0 ? h0 : (jj == 1 ? v1 : (v1 - (jj - 1) * e_ins > 0 ? v1 - (jj - 1) * e_ins : 0)); };
     int hi = EH::kRing ? (qlen < EXT_LDS_COLS - 1 ? qlen : EXT_LDS_COLS - 1) : qlen;   // columns <= hi hold their values
-    if constexpr (EH::kRing) {
-        static_assert(QPre<QA>::v, "the LDS ring runs with the staged (pre-scaled) query");
-        for (j = 0; j <= hi; ++j) eh.init(j, init_h(j), query(j));
-    } else {
-        for (j = 0; j <= hi; ++j) eh.set(j, make_int2(init_h(j), 0));
-    }
+    for (j = 0; j <= hi; ++j) eh.set(j, make_int2(init_h(j), 0));
     max = o.mat_max > 0 ? o.mat_max : 0;
     max_ins = idiv_plus(qlen * max + end_bonus - o_ins, e_ins, 1);
     max_ins = max_ins > 1 ? max_ins : 1;
@@ -1032,12 +1030,10 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
             h1 = h0 - (o_del + e_del * (i + 1));
             if (h1 < 0) h1 = 0;
         } else h1 = 0;
-        if constexpr (EH::kRing) {
-            if (end > hi) {   // materialise the columns the band reaches for the first time
-                if (end - beg >= EXT_LDS_COLS - 1) { *eh.ovf = true; break; }
-                for (j = hi + 1; j <= end; ++j) eh.init(j, init_h(j), query(j));
-                hi = end;
-            }
+        if (EH::kRing && end > hi) {   // materialise the columns the band reaches for the first time
+            if (end - beg >= EXT_LDS_COLS - 1) { *eh.ovf = true; break; }
+            for (j = hi + 1; j <= end; ++j) eh.set(j, make_int2(init_h(j), 0));
+            hi = end;
         }
         cells += (uint64_t)(end > beg ? end - beg : 0);
         // The row reads column j+1 (eh and query) before it stores column j: the two never share a slot
@@ -1046,48 +1042,42 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
         // [beg, end), last non-zero in [beg, end]) are tracked here from the values being stored; every
         // stored h and e is >= 0, so "non-zero" is (h | e) != 0.
         int nzf = beg < end ? end : beg, nzl = -1;   // (the serial scan's start values)
-        if constexpr (EH::kRing) {
-            // LDS ring: each cell first stores the previous cell's column (deferred by one cell), then reads the word of
-            // column j + 2 (h, e and the query base), then computes column j from the word read two cells earlier.  Every
-            // LDS operation of a cell is issued before its arithmetic, and the wait at the next cell's top finds it done.
-            // The deferred store starts as a rewrite of column beg's own word; the read of column end + 1 (a stale slot)
-            // is never used, and the word of column end (read ahead) gives the row-end store its query base.
-            uint32_t wend;
-            if (beg < end) {
-                typename EH::Cur c0 = eh.cur(beg), c1 = eh.adv(c0);
-                uint32_t w0 = eh.at(c0), w1 = eh.at(c1);
-                typename EH::Cur scur = c0;
-                uint32_t sw = w0;
+        if (EH::kRing && pre && beg < end) {
+            // LDS ring: each cell first stores the previous cell's column (deferred by one cell), then reads column
+            // j + 2, then computes column j from values read two cells earlier.  Every LDS operation of a cell is thus
+            // issued before its arithmetic, and the wait at the next cell's top finds them done -- with the store
+            // last in the cell (the loop above), each trip waited out a whole LDS store latency.  The deferred store
+            // starts as a rewrite of column beg's own old value; reads of columns end + 1 (stale slot) and query
+            // index qlen + 1 (inside the staged rows or the ring) are never used.
+            typename EH::Cur c0 = eh.cur(beg), c1 = eh.adv(c0);
+            int2 p0 = eh.at(c0), p1 = eh.at(c1);
+            int q0 = query(beg), q1 = query(beg + 1);
+            typename EH::Cur sc = c0;
+            int2 sv = p0;
 #pragma unroll 2
-                for (j = beg; j < end; ++j) {
-                    eh.put(scur, sw);
-                    const typename EH::Cur c2 = eh.adv(c1);
-                    const uint32_t w2 = eh.at(c2);
-                    int h, M = (int)(w0 & EhRing::HM), e = (int)__builtin_amdgcn_ubfe(w0, 13u, 13u);
-                    const int hx = h1;
-                    M = M ? M + (int)__builtin_amdgcn_ubfe(prof, w0 >> 26, 4u) - 8 : 0;
-                    h = M > e ? M : e;
-                    h = h > f ? h : f;
-                    h1 = h;
-                    mj = m > h ? mj : j;
-                    m = m > h ? m : h;
-                    t = M - oe_del; t = t > 0 ? t : 0;
-                    e -= e_del; e = e > t ? e : t;
-                    scur = c0; sw = (uint32_t)hx | (uint32_t)e << 13 | (w0 & EhRing::QM);
-                    if ((hx | e) != 0) { nzl = j; nzf = nzf < j ? nzf : j; }
-                    t = M - oe_ins; t = t > 0 ? t : 0;
-                    f -= e_ins; f = f > t ? f : t;
-                    w0 = w1; w1 = w2; c0 = c1; c1 = c2;
-                }
-                eh.put(scur, sw);
-                wend = w0;   // column end's word
-            } else {
-                j = beg;
-                wend = eh.word(end);
+            for (j = beg; j < end; ++j) {
+                eh.put(sc, sv);
+                const typename EH::Cur c2 = eh.adv(c1);
+                const int2 p2 = eh.at(c2);
+                const int q2 = query(j + 2);
+                int h, M = p0.x, e = p0.y;
+                const int hx = h1;
+                M = M ? M + (int)__builtin_amdgcn_ubfe(prof, (uint32_t)q0, 4u) - 8 : 0;
+                h = M > e ? M : e;
+                h = h > f ? h : f;
+                h1 = h;
+                mj = m > h ? mj : j;
+                m = m > h ? m : h;
+                t = M - oe_del; t = t > 0 ? t : 0;
+                e -= e_del; e = e > t ? e : t;
+                sc = c0; sv = make_int2(hx, e);
+                if ((hx | e) != 0) { nzl = j; nzf = nzf < j ? nzf : j; }
+                t = M - oe_ins; t = t > 0 ? t : 0;
+                f -= e_ins; f = f > t ? f : t;
+                p0 = p1; p1 = p2; q0 = q1; q1 = q2; c0 = c1; c1 = c2;
             }
-            eh.word(end) = (uint32_t)h1 | (wend & EhRing::QM);   // (h1, e = 0), the query base kept
-        } else {
-        if (beg < end) {
+            eh.put(sc, sv);
+        } else if (beg < end) {
             typename EH::Cur cj = eh.cur(beg);
             int2 p = eh.at(cj);
             int qj = query(beg);
@@ -1115,7 +1105,6 @@ DEV int ksw_extend2_body(const DOpts &o, int qlen, QA query, int tlen, TAcc targ
             }
         } else j = beg;
         eh.set(end, make_int2(h1, 0));
-        }
         if (h1 != 0) nzl = end;
         if (j == qlen) {
             max_ie = gscore > h1 ? max_ie : i;
@@ -2230,7 +2219,7 @@ hipError_t launch_extend(int grid, hipStream_t st, const DIndex &ix, const DOpts
     auto in4 = [](int v) { return v >= -8 && v <= 7; };   // the profile's 4-bit score fields
     const bool lds = !sel && cp.max_len <= 200 && 2 * wb + 2 < 63 && in4(o.mat_match) && in4(o.mat_mismatch) &&
                      in4(o.mat_amb) &&
-                     (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 8000;   // 13-bit h, e
+                     (int64_t)cp.max_len * (2 * (int64_t)o.a + 2 * o.mat_max) + o.pen_clip3 + o.pen_clip5 < 60000;
     // Contiguous per-thread scratch (S = 1).  The lane-interleaved layout (S = 64, as k_chain's) measured slower
     // here: lone 1M-read launch 7.0 ms against 6.67 ms, PMC fetch + write 1.17 GB against 1.28 GB -- the kernel is
     // bound by VALU issue under divergence, not by its scratch traffic.
