@@ -30,7 +30,8 @@ _RCCL_IN_PROCESS = (int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--exchange-wo
                     or "--group-devices" in sys.argv[1:]
                     or any(a.startswith("--gpus") and (a.split("=")[1:] or ["1"])[0] != "1" for a in sys.argv[1:])
                     or ("--gpus" in sys.argv[1:] and sys.argv[sys.argv.index("--gpus") + 1:][:1] != ["1"]))
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSQ_HW_QUEUES", "16" if _RCCL_IN_PROCESS else "8")
+if os.environ.get("BSQ_HW_QUEUES") != "lib":   # "lib": leave the choice to libbsq's load-time default (8 when unset)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSQ_HW_QUEUES", "16" if _RCCL_IN_PROCESS else "8")
 # the native record exchange gives up (and aborts its communicator on every rank) after this long without progress
 # from the other ranks; a timed step is ~20 ms, so 3 minutes means a broken run, and the job should end, not hang
 os.environ.setdefault("BSQ_XCHG_TIMEOUT_S", "180")

@@ -160,6 +160,13 @@ extern "C" const char *bsq_last_error(void) { return g_err.c_str(); }
 // for the other translation units of the library (group.cpp); not part of include/bsq.h
 extern "C" void bsq_internal_set_error(const char *msg) { g_err = msg ? msg : ""; }
 extern "C" const char *bsq_version(void) { return "bsq 0.1 (gfx950)"; }
+
+// The concurrent batch and pipeline streams of one process need more than HIP's default 4 hardware queues: the 4-batch
+// C3 step measured 45 M reads/s on 4 queues against 57 M on 8 (profiles/r06/streams_queues/ab.txt; 16 level with 8).
+// A process that has not chosen gets 8 -- set when the library is loaded, before its first HIP call (the runtime reads
+// the variable when it initialises, on the first HIP call).  An explicit GPU_MAX_HW_QUEUES, or a HIP runtime that
+// another library of the process has already initialised, is left as it is.
+__attribute__((constructor)) static void bsq_default_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "8", 0); }
 extern "C" void bsq_free(void *p) { free(p); }
 
 extern "C" int bsq_device_count(void)
