@@ -32,6 +32,14 @@ _RCCL_IN_PROCESS = (int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--exchange-wo
                     or ("--gpus" in sys.argv[1:] and sys.argv[sys.argv.index("--gpus") + 1:][:1] != ["1"]))
 if os.environ.get("BSQ_HW_QUEUES") != "lib":   # "lib": leave the choice to libbsq's load-time default (8 when unset)
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSQ_HW_QUEUES", "16" if _RCCL_IN_PROCESS else "8")
+# BSQ_REHEARSE_SHARED_GPU=1 (one-GPU rehearsal of the driver's torchrun run, tools/rehearse_rccl.sh): RCCL refuses two ranks on
+# one device ("Duplicate GPU detected", judged by host id + bus id), so every rank claims a host of its own and RCCL
+# connects them over its socket transport on the loopback device -- the native exchange (all-gathers, send/recv of the
+# wire records, rank 0's expansion) then runs for real between processes; rates are meaningless (one shared GPU)
+if os.environ.get("BSQ_REHEARSE_SHARED_GPU") == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ["NCCL_HOSTID"] = "bsq-rehearsal-rank" + os.environ.get("RANK", "0")
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
 # the native record exchange gives up (and aborts its communicator on every rank) after this long without progress
 # from the other ranks; a timed step is ~20 ms, so 3 minutes means a broken run, and the job should end, not hang
 os.environ.setdefault("BSQ_XCHG_TIMEOUT_S", "180")
