@@ -59,7 +59,6 @@ hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, cons
 hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
                           const uint32_t *, uint32_t *, int32_t *, int32_t *);
 bool wide_z32(const DIndex &);
-bool smem_wide_single();
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
 hipError_t launch_kmer_build(hipStream_t, const DIndex &, uint32_t *, int);
@@ -1376,8 +1375,7 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         // 29.0 at 11, 30.4 at 10).  BSQ_TEST_LCAP shrinks the LDS share so the spill path is tested
         // (tests/test_gpu_parity.py).
         const int lcap_env = getenv("BSQ_TEST_LCAP") ? atoi(getenv("BSQ_TEST_LCAP")) : 0;
-        // (BSQ_WIDE_SINGLE: 11 entries of 14 B = 9.9 KB per one-wave block, 16 waves per CU)
-        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : wide_z32(ix) ? (smem_wide_single() ? 11 : 14) : 12;
+        const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : wide_z32(ix) ? 14 : 12;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
         if (st != b->stream) {

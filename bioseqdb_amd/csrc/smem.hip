@@ -312,9 +312,7 @@ struct OutSlot {   // the read's output intervals (global, wave-interleaved), me
     int n, cap, n1;
 };
 
-// P: backward-phase list entries extended in pairs (4 rank blocks in flight per trip); false: one per trip -- 40 fewer
-// VGPRs for 64-bit rows (122 instead of 162), so the kernel fits 4 waves per SIMD
-template <typename X, typename Z, typename Q, bool P = true>
+template <typename X, typename Z, typename Q>
 DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z> &L, OutSlot &S,
                   bool &ovf, uint64_t &nblk, uint64_t &nkm)
 {
@@ -467,7 +465,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
         {
             // entries j and j+1 are extended together (independent); bookkeeping stays in list order.
             // Compaction writes go to nc <= j, below both entries already read.
-            const bool hb = P && j + 1 < n;
+            const bool hb = j + 1 < n;
             X pa0, pb0;
             Z pa2, pb2;
             int pae, pbe;
@@ -509,7 +507,7 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
                 }
             }
         }
-        j += P ? 2 : 1;
+        j += 2;
         if (j >= n) {   // position i done (at i = -1 every entry is a hit, so nc == 0 ends the loop there)
             if (nc == 0) break;
             n = nc; nc = 0; j = 0; last_x2 = 0;
@@ -605,8 +603,8 @@ __global__ void __launch_bounds__(256) k_codes_wave(const uint8_t *codes, const 
 }
 
 // 4 waves per SIMD for u32 rows (16 one-wave blocks per CU, the LDS limit), 3 for 64-bit rows
-template <typename X, typename Z, typename Q, bool P = true>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 || !P ? 4 : 3))) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
+template <typename X, typename Z, typename Q>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(X) == 4 ? 4 : 3))) k_smem_lds(DIndex ix, DOpts o, Caps cp, const uint8_t *codes, const int64_t *offs,
                                                   int n, Intv *intv_out, int32_t *n_intv, uint32_t *status,
                                                   Counters *ctr, int lcap, uint8_t *spill, int gcap, int qcap)
 {
@@ -667,7 +665,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
         int x = 0;
         while (x < len && !ovf) {
             if (q[x] < 4) {
-                x = smem1_lds<X, Z, Q, P>(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
+                x = smem1_lds(fm, len, q, x, 1, L, S, ovf, nblk, nkm);
                 if (!ovf) take_mem1(false);
             } else ++x;
         }
@@ -676,7 +674,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
             const Intv p = S.a[k];
             const int start = (int)(p.info >> 32), end = (int)(uint32_t)p.info;
             if (end - start < split_len || p.x[2] > (uint64_t)o.split_width) continue;
-            smem1_lds<X, Z, Q, P>(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
+            smem1_lds(fm, len, q, (start + end) >> 1, (int)p.x[2] + 1, L, S, ovf, nblk, nkm);
             if (!ovf) take_mem1(true);
         }
         if (o.max_mem_intv > 0) {
@@ -721,13 +719,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
 template <typename X, typename Z>
 static size_t lds_bytes(int threads, int lcap) { return (size_t)threads * lcap * (sizeof(X) + sizeof(Z) + 2); }
 
-// 64-bit rows with u32 interval sizes: backward entries one per trip at 16 waves per CU (BSQ_WIDE_SINGLE=1, experiment)
-bool smem_wide_single()
-{
-    const char *e = getenv("BSQ_WIDE_SINGLE");
-    return e && *e == '1';
-}
-
 // 64-bit rows whose interval sizes fit u32 (every x[2] is at most one base's count, <= l_pac); BSQ_FORCE_WIDE=2
 // (tests) takes the all-u64 kernel on any index
 bool wide_z32(const DIndex &ix)
@@ -751,20 +742,19 @@ hipError_t launch_smem_lds(hipStream_t st, const DIndex &ix, const DOpts &o, con
     const int L = cp.max_len;
     if (codes_t)
         hipLaunchKernelGGL(k_codes_wave, dim3((n + 63) / 64), dim3(256), (size_t)64 * L, st, codes, offs, n, L, codes_t);
-#define BSQ_SMEM_LAUNCH(X_, Z_, P_)                                                                                     \
+#define BSQ_SMEM_LAUNCH(X_, Z_)                                                                                         \
     do {                                                                                                               \
         const size_t sh = lds_bytes<X_, Z_>(T, lcap);                                                                  \
         if (codes_t)                                                                                                   \
-            hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT, P_>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,  \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, QT>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes_t, offs, n,      \
                                intv, n_intv, status, ctr, lcap, spill, gcap, L);                                       \
         else                                                                                                           \
-            hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *, P_>), dim3(grid), dim3(T), sh, st, ix, o, cp,       \
-                               codes, offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                       \
+            hipLaunchKernelGGL((k_smem_lds<X_, Z_, const uint8_t *>), dim3(grid), dim3(T), sh, st, ix, o, cp, codes,    \
+                               offs, n, intv, n_intv, status, ctr, lcap, spill, gcap, L);                              \
     } while (0)
-    if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t, true);
-    else if (wide_z32(ix) && smem_wide_single()) BSQ_SMEM_LAUNCH(uint64_t, uint32_t, false);
-    else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t, true);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
-    else BSQ_SMEM_LAUNCH(uint64_t, uint64_t, true);
+    if (!ix.wide) BSQ_SMEM_LAUNCH(uint32_t, uint32_t);
+    else if (wide_z32(ix)) BSQ_SMEM_LAUNCH(uint64_t, uint32_t);   // 64-bit rows, interval sizes in u32 (l_pac < 2^32)
+    else BSQ_SMEM_LAUNCH(uint64_t, uint64_t);
 #undef BSQ_SMEM_LAUNCH
     return hipGetLastError();
 }
