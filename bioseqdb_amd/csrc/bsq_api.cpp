@@ -886,8 +886,6 @@ struct bsq_batch {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;  // the nuclseq columns (high priority: created on first use)
-    hipStream_t sstream = nullptr;  // BSQ_CU_SPLIT (experiment): main-pass seeding on its own CU set
-    hipEvent_t sev[2]{};
     int32_t max_reads = 0;
     int64_t max_bases = 0;
     int32_t n_reads = 0;
@@ -1026,27 +1024,7 @@ extern "C" int bsq_batch_create(bsq_index *idx, int32_t max_reads, int64_t max_b
     }
     *out = b;
     HIPCHK(hipSetDevice(b->device));
-    if (const char *cs = getenv("BSQ_CU_SPLIT")) {
-        // Experiment: seeding and the DP stages on disjoint CU sets, so one batch's seeding runs beside
-        // the other batches' extension/CIGAR kernels without sharing CUs.  BSQ_CU_SPLIT=s[:mode]: of every 8 CU
-        // indices (mode "mod", the default) or of the first s/8 of all CUs (mode "blk"), s go to seeding.
-        int sp = atoi(cs);
-        const bool blk = strstr(cs, "blk") != nullptr;
-        hipDeviceProp_t pr;
-        HIPCHK(hipGetDeviceProperties(&pr, b->device));
-        const int ncu = pr.multiProcessorCount, words = (ncu + 31) / 32;
-        if (sp > 0 && sp < 8) {
-            std::vector<uint32_t> ms((size_t)words, 0), md((size_t)words, 0);
-            for (int c = 0; c < ncu; ++c) {
-                const bool seed = blk ? c < ncu * sp / 8 : (c % 8) < sp;
-                (seed ? ms : md)[(size_t)(c / 32)] |= 1u << (c % 32);
-            }
-            HIPCHK(hipExtStreamCreateWithCUMask(&b->stream, (uint32_t)words, md.data()));
-            HIPCHK(hipExtStreamCreateWithCUMask(&b->sstream, (uint32_t)words, ms.data()));
-            for (auto &e : b->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-    }
-    if (!b->stream) HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     for (auto &e : b->ev) HIPCHK(hipEventCreate(&e));
     const size_t R = (size_t)std::max(max_reads, 1);
     // whole 16-B words plus one: the reg2aln query stream loads the aligned word holding a read's last base
@@ -1094,8 +1072,6 @@ extern "C" void bsq_batch_free(bsq_batch *b)
         hipSetDevice(b->device);
     }
     if (b->stream) hipStreamDestroy(b->stream);
-    if (b->sstream) hipStreamDestroy(b->sstream);
-    for (auto &e : b->sev) if (e) hipEventDestroy(e);
     if (b->cstream && b->cstream != b->stream) { hipStreamSynchronize(b->cstream); hipStreamDestroy(b->cstream); }
     delete b;
 }
@@ -1361,11 +1337,6 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
 {
     const DIndex &ix = b->idx->h.dev->view;
     hipStream_t st = b->stream;
-    if (b->sstream && !sel && w.cp.max_len < 65536) {   // BSQ_CU_SPLIT: the main pass on the seeding CU set
-        HIPCHK(hipEventRecord(b->sev[0], b->stream));
-        HIPCHK(hipStreamWaitEvent(b->sstream, b->sev[0], 0));
-        st = b->sstream;
-    }
     if (!sel && w.cp.max_len < 65536) {
         // main pass: LDS-resident SMEM lists (smem.hip); overflowing reads fall through to the retry pass
         // u32 rows: 15 entries in LDS = 9.6 KB per one-wave block, 16 waves per CU; longer lists spill.
@@ -1378,10 +1349,6 @@ static int seed_stage(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int lcap = tiny_caps() ? 3 : lcap_env > 0 ? lcap_env : !ix.wide ? 15 : wide_z32(ix) ? 14 : 12;
         HIPCHK(launch_smem_lds(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.intv, w.n_intv, w.status, b->ctr, lcap,
                                w.lspill, tiny_caps() ? 0 : LSPILL, w.codes_t));
-        if (st != b->stream) {
-            HIPCHK(hipEventRecord(b->sev[1], st));
-            HIPCHK(hipStreamWaitEvent(b->stream, b->sev[1], 0));
-        }
     } else {
         HIPCHK(launch_smem(w.grid, st, ix, o, w.cp, b->codes, (b->offs + b->lo), sel, n, w.intv, w.n_intv, w.status, w.scratch, b->ctr));
     }
