@@ -56,8 +56,6 @@ hipError_t launch_reg2aln_chain(hipStream_t, const DIndex &, const DOpts &, cons
                                 const int64_t *, int, const Reg *, const int32_t *, Hit *, uint32_t *, int32_t *,
                                 uint32_t *, Counters *, int, uint8_t *, int64_t, int, int32_t *, int32_t *, int32_t *,
                                 const int32_t *, const int32_t *, int32_t *);
-hipError_t launch_r2a_key(hipStream_t, const DOpts &, const Caps &, const int64_t *, int, const Reg *, const int32_t *,
-                          const uint32_t *, uint32_t *, int32_t *, int32_t *);
 bool wide_z32(const DIndex &);
 hipError_t launch_smem_lds(hipStream_t, const DIndex &, const DOpts &, const Caps &, const uint8_t *, const int64_t *, int,
                            Intv *, int32_t *, uint32_t *, Counters *, int, uint8_t *, int, uint8_t *);
@@ -1392,18 +1390,13 @@ static int run_stages(bsq_batch *b, Workspace &w, const DOpts &o, int n, const i
         const int64_t q_bytes = ((int64_t)w.cp.max_len + 16) & ~15LL;
         const int zcap = (int)std::max<int64_t>(4096, (int64_t)(150 * 1024 / 12) - (int64_t)eh_bytes - q_bytes) & ~15;
         // persistent waves (3 blocks of 4 waves per CU); each owns a global traceback slab for big bands
-        const int32_t *r_order = nullptr;
-        if (w.ekey0) {
-            // group balance: reads in order of their band class (the extension's sort buffers are free now)
-            HIPCHK(launch_r2a_key(st, o, w.cp, (b->offs + b->lo), n, w.regs, w.n_regs, w.status, w.ekey0, w.eidx0, w.dcount + 2));
-            size_t tb = w.esort_bytes;
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.esort_tmp, tb, w.ekey0, w.ekey1, w.eidx0, w.eidx1, n, 0, 3, st));
-            r_order = w.eidx1;
-        }
+        // The diagonal pass takes the reads in batch order and routes each one it does not decide to the kernel of its
+        // widest first band.  (Ordering the pass by that band class first -- a key kernel and a 3-bit sort -- measured
+        // level: C3 step 56.7 / 56.3 / 57.2 M against 56.7 / 56.4 / 57.5 M without; profiles/r06/r2a_order/.)
         HIPCHK(launch_reg2aln_chain(st, ix, o, w.cp, b->codes, (b->offs + b->lo), n, w.regs, w.n_regs, w.hits, w.cigars, w.n_cig,
                                     w.status, b->ctr, tiny_caps() ? 64 : zcap, w.zslab, w.zslab_bytes, w.zslab_blocks,
-                                    w.dlist0, w.dlist1, w.dcount, r_order, r_order ? w.dcount + 2 : nullptr,
-                                    r_order && !no_r2a_diag() ? w.eidx0 : nullptr));
+                                    w.dlist0, w.dlist1, w.dcount, nullptr, nullptr,
+                                    w.eidx0 && !no_r2a_diag() ? w.eidx0 : nullptr));
         if (getenv("BSQ_R2A_COUNTS")) {   // diagnostics: reads handed on by each reg2aln kernel (host sync)
             int32_t dc[4] = {0, 0, 0, 0};
             HIPCHK(hipMemcpyAsync(dc, w.dcount, sizeof dc, hipMemcpyDeviceToHost, st));

@@ -906,55 +906,6 @@ static hipError_t launch_g(hipStream_t st, const DIndex &ix, const DOpts &o, con
     return hipGetLastError();
 }
 
-// Sort key of a read for mem_reg2aln: the widest first-iteration band class over its regions
-// (0: exact, no DP; 1: <= 16 columns; 2: <= 32; 3: <= 64; 4: wider), so each group-mode wave holds
-// reads of one class.  Only the processing order depends on it.
-__global__ void k_r2a_key(DOpts o, Caps cp, const int64_t *__restrict__ offs, int n, const Reg *__restrict__ regs,
-                          const int32_t *__restrict__ n_regs, const uint32_t *__restrict__ status,
-                          uint32_t *__restrict__ key, int32_t *__restrict__ idx, int32_t *__restrict__ n_out)
-{
-    const int li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li == 0) *n_out = n;
-    if (li >= n) return;
-    uint32_t cls = 0;
-    if (!status[li]) {
-        const int nr = n_regs[li];
-        for (int g = 0; g < nr; ++g) {
-            const Reg &ar = regs[(size_t)li * cp.regs + g];
-            const int lq = ar.qe - ar.qb;
-            const int64_t rl = ar.re - ar.rb;
-            int tmp = infer_bw(lq, (int)rl, ar.truesc, o.a, o.o_del, o.e_del);
-            int w2 = infer_bw(lq, (int)rl, ar.truesc, o.a, o.o_ins, o.e_ins);
-            w2 = w2 > tmp ? w2 : tmp;
-            if (w2 > o.w) w2 = w2 < ar.w ? w2 : ar.w;
-            w2 = w2 < o.w << 2 ? w2 : o.w << 2;
-            uint32_t c;
-            if (lq == rl && w2 == 0) c = 0;
-            else {
-                int mg = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_ins, o.e_ins, 1);
-                int md = idiv_plus(((lq + 1) >> 1) * o.mat_match - o.o_del, o.e_del, 1);
-                mg = mg > md ? mg : md; mg = mg > 1 ? mg : 1;
-                int dl = (int)rl - lq; dl = dl < 0 ? -dl : dl;
-                int ww = (mg + dl + 1) >> 1; ww = ww < w2 ? ww : w2; ww = ww > dl + 3 ? ww : dl + 3;
-                const int nc = lq < 2 * ww + 1 ? lq : 2 * ww + 1;
-                c = nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 3 : 4;
-            }
-            cls = cls > c ? cls : c;
-        }
-    }
-    key[li] = cls;
-    idx[li] = li;
-}
-
-hipError_t launch_r2a_key(hipStream_t st, const DOpts &o, const Caps &cp, const int64_t *offs, int n, const Reg *regs,
-                          const int32_t *n_regs, const uint32_t *status, uint32_t *key, int32_t *idx, int32_t *n_out)
-{
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_r2a_key, dim3((n + 255) / 256), dim3(256), 0, st, o, cp, offs, n, regs, n_regs, status, key,
-                       idx, n_out);
-    return hipGetLastError();
-}
-
 // ================================================================================================
 // Diagonal pass: one lane per read.  Most regions of 150-bp reads are gapless with a few mismatches, and
 // bwa_gen_cigar2 returns "nM" for them without a DP (w == 0, diagonal_wins, or the exact detour test).  This
@@ -1025,7 +976,7 @@ DEV bool diag_decides(const DIndex &ix, const DOpts &o, const Score sc, int w_, 
     return (int64_t)sum > bound2 && (int64_t)x < (int64_t)(o.o_ins + o.e_ins + o.o_del + o.e_del);
 }
 
-// mem_reg2aln's first band of a region as k_r2a_key classes it: 1 (<= 16 columns), 2 (<= 32) or 3 (wider)
+// mem_reg2aln's first band of a region: class 1 (<= 16 columns), 2 (<= 32) or 3 (wider)
 DEV int band_class(const DOpts &o, int lq, int64_t rl, int w2)
 {
     if (lq <= 0 || rl <= 0 || rl > (1 << 30)) return 1;   // gen_cigar2's early exits: no DP in any kernel
@@ -1048,9 +999,9 @@ DEV void wave_append(bool on, int li, int32_t *list, int32_t *count)
     if (on) list[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = li;
 }
 
-// Reads with a region the pass does not decide go straight to the kernel of their widest first band (the class
-// k_r2a_key sorts by): <= 16 columns to `defer` (k_reg2aln_g<16>'s input), <= 32 to d0 (k_reg2aln_g<32>'s), wider
-// to d1 (k_reg2aln_w's) -- each kernel recomputes a read from scratch and still defers what outgrows it.
+// Reads with a region the pass does not decide go straight to the kernel of their widest first band: <= 16 columns
+// to `defer` (k_reg2aln_g<16>'s input), <= 32 to d0 (k_reg2aln_g<32>'s), wider to d1 (k_reg2aln_w's) -- each kernel
+// recomputes a read from scratch and still defers what outgrows it.
 __global__ void __launch_bounds__(256) k_reg2aln_diag(DIndex ix, DOpts o, Caps cp, const uint8_t *__restrict__ codes,
                                                       const int64_t *__restrict__ offs, int n,
                                                       const int32_t *__restrict__ list, const int32_t *__restrict__ list_n,
