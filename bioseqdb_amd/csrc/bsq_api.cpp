@@ -334,10 +334,11 @@ static int kmer_depth(uint64_t seq_len, bool wide)
     // competes with them for it (C3, 100 MB of rank blocks: seeding 10.45 ms at K = 10 with a 22 MB table, 10.7 at
     // 11 with 89 MB, 11.3-12.1 at 12-14, 10.9 at 9); else at most 13: the rank blocks' lines miss anyway and each
     // level answers more backward extensions with one line (C4, 3 Gbp: 28.0 M reads/s at 11, 30.0 M at 13 with a
-    // 2.9 GB table).  Depth 13 only for 64-bit rows, the kernels that preload 13 levels
-    // (and the only ones measured there): u32 rows of a 256 Mbp - 2 Gbp text stay at 10, where u32 kernels preload
-    // 11 levels and read deeper ones one per step (slower at C3: 11.3-12.1 ms against 10.45).
-    const int kmax = wide && seq_len / 2 > (256ull << 20) ? 13 : 10;
+    // 2.9 GB table, round 5; 32.5 M at 15 with a 46 GB table against 31.7 M at 13, round 6).
+    // Depth 15 only for 64-bit rows, the kernels that preload 15 levels (and the only ones measured there; the table
+    // is at most 46 GB beside a >= 8 GB suffix array): u32 rows of a 256 Mbp - 2 Gbp text stay at 10, where u32
+    // kernels preload 11 levels and read deeper ones one per step (slower at C3: 11.3-12.1 ms against 10.45).
+    const int kmax = wide && seq_len / 2 > (256ull << 20) ? 15 : 10;
     int K = 0;
     while (K < kmax && (1ull << (2 * (K + 1))) <= seq_len) ++K;
     // BSQ_KMER_K: 0 disables; up to 15 (the kernels preload levels <= 11 and read deeper levels one per step;

@@ -332,9 +332,10 @@ DEV int smem1_lds(const FM<X> &fm, int len, Q q, int x, int min_intv, LList<X, Z
         // the walk below then consumes them in order with the exact bookkeeping of the loop that follows.
         // (64-bit rows too: at 3 Gbp the table is a 179 MB array whose rows miss the caches as often as not,
         // and K - 1 dependent round trips per SMEM call were a fifth of the seeding kernel's time.)
-        // rows preloaded: 11, or 13 for 64-bit rows (whose table is 13 deep: C4); a deeper table (kmer_depth up to
-        // 15) serves lengths KM+1..K one per step below
-        constexpr int KM = sizeof(X) == 8 ? 13 : 11;
+        // rows preloaded: 11, or 15 for 64-bit rows (whose table is 15 deep: C4; 162 VGPRs as with 13, and the C4
+        // step 31.7 -> 32.5 M reads/s against 13 levels); a table deeper than KM
+        // (BSQ_KMER_K up to 15 for u32 rows) serves lengths KM+1..K one per step below
+        constexpr int KM = sizeof(X) == 8 ? 15 : 11;
         const int Kp = fm.K < KM ? fm.K : KM;
         const int Lt = Kp < len - x ? Kp : len - x;
         int cb[KM + 1];

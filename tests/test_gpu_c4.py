@@ -1,7 +1,7 @@
 """C4 (BASELINE.json configs[3]) under GPU parity: the bench's 3 Gbp synthetic reference, 24 rows x 125 Mbp.
 
 At 2 x 3e9 = 6e9 suffixes the index takes the 64-bit-row path for real (u64 suffix array, u64 SMEM lists,
-k-mer table at K = 13 -- levels past 11 read one per step -- occ blocks of a 3 GB BWT outside the Infinity Cache).  The reference itself cannot
+k-mer table at K = 15, all 15 levels preloaded per SMEM call -- occ blocks of a 3 GB BWT outside the Infinity Cache).  The reference itself cannot
 build this index at all (is_bwt takes an int length: bioseqdb/bwa.cpp:10,47; rows are capped at
 INT32_MAX/4 bases: extension.cpp:50), so the oracle is the only check.  Its FM tables are derived on the host
 from the GPU-built suffix array once that SA has passed two certificates, each a proof that it is the unique SA

@@ -140,12 +140,12 @@ def test_parity_wide_rows(monkeypatch, force, lcap):
     assert not bad, bad[:20]
 
 
-@pytest.mark.parametrize("force,k", [("0", "13"), ("1", "13"), ("2", "13"), ("0", "0")],
-                         ids=["u32_k13", "z32_k13", "z64_k13", "no_table"])
+@pytest.mark.parametrize("force,k", [("0", "13"), ("1", "13"), ("2", "13"), ("1", "15"), ("2", "15"), ("0", "0")],
+                         ids=["u32_k13", "z32_k13", "z64_k13", "z32_k15", "z64_k15", "no_table"])
 def test_parity_kmer_table_depth(monkeypatch, force, k):
-    """k-mer tables deeper than the 11 levels the seeding kernels preload (levels past 11 read one per step in the
-    forward loop, the seed strategy and the backward phase; the C4 default is 13) and no table at all give the
-    oracle's rows.  BSQ_KMER_K forces the depth on a small reference (the default here is 10)."""
+    """k-mer tables deeper than the 11 levels the u32-row kernels preload (levels past 11 read one per step in the
+    forward loop, the seed strategy and the backward phase), the 64-bit-row kernels at 13 levels (a partial preload) and
+    at 15 (all levels preloaded; the C4 default; a 46 GB table), and no table at all give the oracle's rows.  BSQ_KMER_K forces the depth on a small reference (the default here is 10)."""
     monkeypatch.setenv("BSQ_KMER_K", k)
     if force != "0":
         monkeypatch.setenv("BSQ_FORCE_WIDE", force)
